@@ -1,0 +1,145 @@
+"""ctypes loader for the C restatement (oracle/cfd_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — never by the product package cfd-demo_amd/.
+PARITY UNPINNED against the reference itself (see cfd_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libcfd_oracle.so")
+
+FIELDS = ["u", "v", "p", "u_old", "v_old", "u_star", "v_star", "rhs", "p_prime", "p_prime_new"]
+
+
+class OrcGrid(C.Structure):
+    _fields_ = [("nx", C.c_uint64), ("ny", C.c_uint64), ("lx", C.c_float), ("ly", C.c_float),
+                ("has_cylinder", C.c_int32), ("cx", C.c_float), ("cy", C.c_float),
+                ("radius", C.c_float)]
+
+
+class OrcParams(C.Structure):
+    _fields_ = [("dt", C.c_float), ("viscosity", C.c_float),
+                ("target_inlet_velocity", C.c_float), ("scheme", C.c_int32),
+                ("inlet_profile", C.c_int32), ("pressure_solver", C.c_int32),
+                ("jacobi_iters", C.c_int32), ("corrector_passes", C.c_int32),
+                ("tol_enabled", C.c_int32), ("p_tol", C.c_float), ("bc_kind", C.c_int32)]
+
+
+class OrcScalars(C.Structure):
+    _fields_ = [("step", C.c_uint64), ("time", C.c_float), ("dt", C.c_float), ("p", C.c_float),
+                ("u", C.c_float), ("v", C.c_float), ("current_inlet_velocity", C.c_float),
+                ("jacobi_sweeps_total", C.c_uint64)]
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.orc_create.restype = C.c_void_p
+        L.orc_create.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcParams)]
+        L.orc_destroy.argtypes = [C.c_void_p]
+        L.orc_set_params.argtypes = [C.c_void_p, C.POINTER(OrcParams)]
+        for name in ("orc_update", "orc_boundary_conditions"):
+            getattr(L, name).argtypes = [C.c_void_p]
+        for name in ("orc_piso_step", "orc_u_predictor", "orc_v_predictor", "orc_divergence",
+                     "orc_corrector"):
+            getattr(L, name).argtypes = [C.c_void_p, C.c_float]
+        L.orc_jacobi_pressure.argtypes = [C.c_void_p]
+        L.orc_jacobi_pressure.restype = C.c_float
+        L.orc_auto_dt.argtypes = [C.c_void_p]
+        L.orc_auto_dt.restype = C.c_float
+        L.orc_field.argtypes = [C.c_void_p, C.c_int]
+        L.orc_field.restype = C.POINTER(C.c_float)
+        L.orc_field_len.argtypes = [C.c_void_p, C.c_int]
+        L.orc_field_len.restype = C.c_size_t
+        L.orc_mask.argtypes = [C.c_void_p, C.c_int]
+        L.orc_mask.restype = C.POINTER(C.c_uint8)
+        L.orc_get_scalars.argtypes = [C.c_void_p, C.POINTER(OrcScalars)]
+        L.orc_set_scalars.argtypes = [C.c_void_p, C.POINTER(OrcScalars)]
+        _lib = L
+    return _lib
+
+
+def make_params(dt=0.005, viscosity=1e-6, target_inlet_velocity=1.0, scheme=0, inlet_profile=0,
+                jacobi_iters=50, corrector_passes=20, tol_enabled=1, p_tol=1e-4, bc_kind=0):
+    return OrcParams(dt, viscosity, target_inlet_velocity, scheme, inlet_profile, 0,
+                     jacobi_iters, corrector_passes, int(tol_enabled), p_tol, bc_kind)
+
+
+class OracleModel:
+    """Thin handle over orc_model; fields are exposed as numpy views."""
+
+    def __init__(self, nx, ny, lx, ly, cylinder=None, **params):
+        g = OrcGrid(nx, ny, lx, ly, 1 if cylinder else 0,
+                    *(cylinder if cylinder else (0.0, 0.0, 0.0)))
+        self.nx, self.ny = nx, ny
+        self._p = make_params(**params)
+        self.h = lib().orc_create(C.byref(g), C.byref(self._p))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    def field(self, name: str) -> np.ndarray:
+        k = FIELDS.index(name)
+        n = lib().orc_field_len(self.h, k)
+        return np.ctypeslib.as_array(lib().orc_field(self.h, k), shape=(n,))
+
+    def mask(self, which: str) -> np.ndarray:
+        k = 0 if which == "u" else 1
+        n = lib().orc_field_len(self.h, 0 if which == "u" else 1)
+        return np.ctypeslib.as_array(lib().orc_mask(self.h, k), shape=(n,))
+
+    def scalars(self) -> OrcScalars:
+        s = OrcScalars()
+        lib().orc_get_scalars(self.h, C.byref(s))
+        return s
+
+    def set_scalars(self, s: OrcScalars):
+        lib().orc_set_scalars(self.h, C.byref(s))
+
+    def set_params(self, **params):
+        self._p = make_params(**params)
+        lib().orc_set_params(self.h, C.byref(self._p))
+
+    def update(self):
+        lib().orc_update(self.h)
+
+    def piso_step(self, dt):
+        lib().orc_piso_step(self.h, dt)
+
+    def u_predictor(self, dt):
+        lib().orc_u_predictor(self.h, dt)
+
+    def v_predictor(self, dt):
+        lib().orc_v_predictor(self.h, dt)
+
+    def divergence(self, dt):
+        lib().orc_divergence(self.h, dt)
+
+    def jacobi(self) -> float:
+        return lib().orc_jacobi_pressure(self.h)
+
+    def corrector(self, dt):
+        lib().orc_corrector(self.h, dt)
+
+    def boundary(self):
+        lib().orc_boundary_conditions(self.h)
