@@ -1,0 +1,402 @@
+"""cfdamd — host-side mirror of cfd-demo's `Model` interface
+(/root/reference/src/model.rs) over the MI355X C ABI (include/cfd.h).
+
+Names, defaults and argument meaning follow the reference:
+
+    SimulationParams / VelocityScheme / InletProfile / PressureSolver  model.rs:13-21, 44-55, 141-159
+    Grid / Cylinder                                                  model.rs:119-139
+    Model.new / update / set_parameters / get_snapshot /
+    get_residuals / run                                              model.rs:219, 304, 1250-1332
+    SimulationControlHandle (stop, pause, resume, set_params,
+    request_snapshot, get_last_available_snapshot,
+    get_new_log_messages)                                            model.rs:57-117
+
+Every call goes to the HIP library; there is no CPU fallback.  Fields are
+returned as float32 numpy arrays in the reference's flat layout.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import CfdError, CfdGrid, CfdParams, CfdResiduals, CfdState, check, load
+
+__all__ = [
+    "VelocityScheme", "InletProfile", "PressureSolver", "BoundaryKind", "Cylinder", "Grid",
+    "SimulationParams", "Residuals", "SimSnapshot", "Model", "SimulationControlHandle",
+    "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "load",
+]
+
+
+class VelocityScheme(enum.IntEnum):          # model.rs:141-146
+    FirstOrder = 0
+    SecondOrder = 1
+
+
+class InletProfile(enum.IntEnum):            # model.rs:154-159
+    Uniform = 0
+    Parabolic = 1
+
+
+class PressureSolver(enum.IntEnum):          # model.rs:148-152
+    Jacobi = 0
+
+
+class BoundaryKind(enum.IntEnum):            # build-defined
+    Channel = 0
+    Cavity = 1
+
+
+@dataclass
+class Cylinder:                              # model.rs:133-139
+    center_x: float
+    center_y: float
+    radius: float
+
+
+@dataclass
+class Grid:                                  # model.rs:119-131
+    nx: int
+    ny: int
+    lx: float
+    ly: float
+    obstacle: Optional[Cylinder] = None
+
+    @property
+    def dx(self) -> float:
+        return float(np.float32(self.lx) / np.float32(self.nx))
+
+    @property
+    def dy(self) -> float:
+        return float(np.float32(self.ly) / np.float32(self.ny))
+
+    def _c(self) -> CfdGrid:
+        o = self.obstacle
+        return CfdGrid(self.nx, self.ny, self.lx, self.ly, 1 if o else 0,
+                       o.center_x if o else 0.0, o.center_y if o else 0.0,
+                       o.radius if o else 0.0)
+
+
+def default_grid() -> Grid:
+    """src/app.rs:32-53."""
+    lx, ly = 30.0, 10.0
+    return Grid(800, 264, lx, ly, Cylinder(lx / 4.0, ly / 2.0, 0.75))
+
+
+def cavity_grid(nx: int, ny: Optional[int] = None) -> Grid:
+    """Build-defined lid-driven cavity: unit height, dx = dy."""
+    ny = nx if ny is None else ny
+    return Grid(nx, ny, float(nx) / float(ny), 1.0, None)
+
+
+@dataclass
+class SimulationParams:                      # model.rs:13-21, defaults :44-55
+    dt: float = 0.005
+    viscosity: float = 0.000001
+    target_inlet_velocity: float = 1.0
+    velocity_scheme: VelocityScheme = VelocityScheme.FirstOrder
+    inlet_profile: InletProfile = InletProfile.Uniform
+    pressure_solver: PressureSolver = PressureSolver.Jacobi
+    # build knobs; reference behaviour by default
+    jacobi_iters: int = 50                   # model.rs:737
+    corrector_passes: int = 20               # model.rs:696
+    tol_enabled: bool = True                 # model.rs:816, 721
+    p_tol: float = 1e-4                      # model.rs:736
+    bc_kind: BoundaryKind = BoundaryKind.Channel
+
+    def _c(self) -> CfdParams:
+        return CfdParams(self.dt, self.viscosity, self.target_inlet_velocity,
+                         int(self.velocity_scheme), int(self.inlet_profile),
+                         int(self.pressure_solver), self.jacobi_iters, self.corrector_passes,
+                         1 if self.tol_enabled else 0, self.p_tol, int(self.bc_kind))
+
+    @staticmethod
+    def cavity(reynolds: float, iters: int, lid: float = 1.0, **kw) -> "SimulationParams":
+        """Lid-driven cavity, nu = U L / Re with L = 1."""
+        return SimulationParams(viscosity=lid * 1.0 / reynolds, target_inlet_velocity=lid,
+                                jacobi_iters=iters, bc_kind=BoundaryKind.Cavity, **kw)
+
+
+@dataclass
+class Residuals:                             # model.rs:23-32
+    simulation_step: int
+    simulation_time: float
+    dt: float
+    p: float
+    u: float
+    v: float
+    step_time: float                         # seconds (device time, HIP events)
+    piso_substeps: int
+    jacobi_sweeps_total: int = 0
+
+
+@dataclass
+class SimSnapshot:                           # model.rs:36-42
+    p: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    dt: float
+    paused: bool = False
+
+
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    check("cfd_rccl_unique_id", load().cfd_rccl_unique_id(buf))
+    return buf.raw
+
+
+def _fp(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Model:
+    """`Model` (model.rs:166-214) with its fields resident in HBM."""
+
+    def __init__(self, grid: Grid, params: SimulationParams, device: int = 0, *,
+                 n_ranks: int = 1, rank: int = 0, unique_id: Optional[bytes] = None):
+        L = load()
+        self.grid = grid
+        self.params = params
+        self._h = C.c_void_p()
+        g, p = grid._c(), params._c()
+        if n_ranks == 1:
+            check("cfd_create", L.cfd_create(C.byref(g), C.byref(p), device, C.byref(self._h)))
+        else:
+            check("cfd_create_sharded",
+                  L.cfd_create_sharded(C.byref(g), C.byref(p), device, n_ranks, rank,
+                                       unique_id, C.byref(self._h)))
+        j0, j1 = C.c_uint64(), C.c_uint64()
+        check("cfd_get_slab", L.cfd_get_slab(self._h, C.byref(j0), C.byref(j1)))
+        self.j0, self.j1 = int(j0.value), int(j1.value)
+        self.n_ranks, self.rank = n_ranks, rank
+
+    @classmethod
+    def new(cls, grid: Grid, params: SimulationParams, device: int = 0) -> "Model":
+        return cls(grid, params, device)
+
+    # ---------------------------------------------------------------- sizes
+    @property
+    def nyl(self) -> int:
+        return self.j1 - self.j0
+
+    def _sizes(self):
+        nx, nyl = self.grid.nx, self.nyl
+        return (nx + 1) * nyl, nx * (nyl + 1), nx * nyl
+
+    # ----------------------------------------------------------------- step
+    def update(self) -> None:
+        """Model::update (model.rs:304-379); asynchronous."""
+        check("cfd_update", load().cfd_update(self._h))
+
+    def update_n(self, n: int) -> None:
+        check("cfd_update_n", load().cfd_update_n(self._h, n))
+
+    def piso_step(self, dt_sub: float) -> None:
+        check("cfd_piso_step", load().cfd_piso_step(self._h, dt_sub))
+
+    def jacobi_pressure(self) -> float:
+        """jacobi_pressure (model.rs:734-824) on the current rhs / p'."""
+        r = C.c_float()
+        check("cfd_pressure_solve", load().cfd_pressure_solve(self._h, C.byref(r)))
+        return float(r.value)
+
+    def run_phase(self, phase: int, dt_sub: float) -> None:
+        check("cfd_run_phase", load().cfd_run_phase(self._h, phase, dt_sub))
+
+    def synchronize(self) -> None:
+        check("cfd_synchronize", load().cfd_synchronize(self._h))
+
+    # --------------------------------------------------------------- params
+    def set_parameters(self, params: SimulationParams) -> None:
+        """set_parameters (model.rs:1250-1257)."""
+        p = params._c()
+        check("cfd_set_params", load().cfd_set_params(self._h, C.byref(p)))
+        self.params = params
+
+    # ---------------------------------------------------------------- reads
+    def get_snapshot(self) -> SimSnapshot:
+        """get_snapshot (model.rs:1259-1267)."""
+        su, sv, sp = self._sizes()
+        u, v, p = (np.empty(n, np.float32) for n in (su, sv, sp))
+        dt = C.c_float()
+        check("cfd_get_snapshot",
+              load().cfd_get_snapshot(self._h, _fp(u), _fp(v), _fp(p), C.byref(dt)))
+        return SimSnapshot(p=p, u=u, v=v, dt=float(dt.value))
+
+    def get_residuals(self) -> Residuals:
+        """get_residuals (model.rs:1269-1280)."""
+        r = CfdResiduals()
+        check("cfd_get_residuals", load().cfd_get_residuals(self._h, C.byref(r)))
+        return Residuals(int(r.simulation_step), float(r.simulation_time), float(r.dt),
+                         float(r.p), float(r.u), float(r.v), float(r.step_time_s),
+                         int(r.piso_substeps), int(r.jacobi_sweeps_total))
+
+    def get_state(self) -> dict:
+        su, sv, sp = self._sizes()
+        arrs = {k: np.empty(n, np.float32) for k, n in
+                (("u", su), ("v", sv), ("p", sp), ("u_star", su), ("v_star", sv),
+                 ("p_prime", sp), ("rhs", sp))}
+        st = CfdState(*(_fp(arrs[k]) for k in ("u", "v", "p", "u_star", "v_star", "p_prime",
+                                               "rhs")))
+        check("cfd_get_state", load().cfd_get_state(self._h, C.byref(st)))
+        arrs.update(dt=np.float32(st.dt), simulation_time=np.float32(st.simulation_time),
+                    simulation_step=int(st.simulation_step),
+                    last_p_residual=np.float32(st.last_p_residual),
+                    last_u_residual=np.float32(st.last_u_residual),
+                    last_v_residual=np.float32(st.last_v_residual),
+                    jacobi_sweeps_total=int(st.jacobi_sweeps_total))
+        return arrs
+
+    def set_state(self, **kw) -> None:
+        """Inject fields/scalars (any subset); others keep their values."""
+        cur = self.get_state()
+        arrs = {}
+        for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
+            a = kw.get(k, cur[k])
+            arrs[k] = np.ascontiguousarray(a, dtype=np.float32)
+            if arrs[k].size != cur[k].size:
+                raise ValueError(f"{k}: expected {cur[k].size} values, got {arrs[k].size}")
+        st = CfdState(*(_fp(arrs[k]) for k in ("u", "v", "p", "u_star", "v_star", "p_prime",
+                                               "rhs")))
+        st.dt = float(kw.get("dt", cur["dt"]))
+        st.simulation_time = float(kw.get("simulation_time", cur["simulation_time"]))
+        st.simulation_step = int(kw.get("simulation_step", cur["simulation_step"]))
+        st.last_p_residual = float(kw.get("last_p_residual", cur["last_p_residual"]))
+        st.last_u_residual = float(kw.get("last_u_residual", cur["last_u_residual"]))
+        st.last_v_residual = float(kw.get("last_v_residual", cur["last_v_residual"]))
+        st.jacobi_sweeps_total = int(kw.get("jacobi_sweeps_total", cur["jacobi_sweeps_total"]))
+        check("cfd_set_state", load().cfd_set_state(self._h, C.byref(st)))
+
+    def get_masks(self):
+        su, sv, _ = self._sizes()
+        mu, mv = np.empty(su, np.uint8), np.empty(sv, np.uint8)
+        check("cfd_get_masks", load().cfd_get_masks(
+            self._h, mu.ctypes.data_as(C.POINTER(C.c_uint8)),
+            mv.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return mu, mv
+
+    # --------------------------------------------------------------- timing
+    def profile_sweeps(self, n: int) -> float:
+        ms = C.c_double()
+        check("cfd_profile_sweeps", load().cfd_profile_sweeps(self._h, n, C.byref(ms)))
+        return float(ms.value)
+
+    def timing_begin(self) -> None:
+        check("cfd_timing_begin", load().cfd_timing_begin(self._h))
+
+    def timing_end(self):
+        a, b, c, d = C.c_double(), C.c_uint64(), C.c_double(), C.c_uint64()
+        check("cfd_timing_end", load().cfd_timing_end(self._h, C.byref(a), C.byref(b),
+                                                      C.byref(c), C.byref(d)))
+        return {"solve_ms": a.value, "sweeps": int(b.value), "step_ms": c.value,
+                "steps": int(d.value)}
+
+    @property
+    def halo_depth(self) -> int:
+        return int(load().cfd_get_halo_depth(self._h))
+
+    # ------------------------------------------------------------------ run
+    def run(self) -> "SimulationControlHandle":
+        """Model::run (model.rs:1282-1332): a worker thread owns the model and
+        steps it while draining commands."""
+        return SimulationControlHandle(self)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            load().cfd_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SimulationControlHandle:
+    """model.rs:65-117 — command channel into the worker thread plus
+    snapshot / residual channels out of it."""
+
+    def __init__(self, model: Model):
+        self._cmd: "queue.Queue" = queue.Queue()
+        self._snap: "queue.Queue" = queue.Queue()
+        self._res: "queue.Queue" = queue.Queue()
+        self._model = model
+        self._thread = threading.Thread(target=self._loop, daemon=True)
+        self._thread.start()
+
+    def _loop(self):                                           # model.rs:1287-1325
+        m, paused, stop = self._model, False, False
+        while not stop:
+            snapshot_sent = False
+            while True:
+                try:
+                    cmd, arg = self._cmd.get_nowait()
+                except queue.Empty:
+                    break
+                if cmd == "stop":
+                    stop = True
+                    break
+                if cmd == "params":
+                    m.set_parameters(arg)
+                elif cmd == "snapshot" and not snapshot_sent:
+                    s = m.get_snapshot()
+                    s.paused = paused
+                    self._snap.put(s)
+                    snapshot_sent = True
+                elif cmd == "pause":
+                    paused = True
+                elif cmd == "resume":
+                    paused = False
+            if stop:
+                break
+            if not paused:
+                m.update()
+                self._res.put(m.get_residuals())
+            else:
+                time.sleep(0.016)
+
+    def stop(self):
+        self._cmd.put(("stop", None))
+
+    def join(self, timeout=None):
+        self._thread.join(timeout)
+
+    def get_last_available_snapshot(self) -> Optional[SimSnapshot]:
+        last = None
+        while True:
+            try:
+                last = self._snap.get_nowait()
+            except queue.Empty:
+                return last
+
+    def get_new_log_messages(self) -> List[Residuals]:
+        out = []
+        while True:
+            try:
+                out.append(self._res.get_nowait())
+            except queue.Empty:
+                return out
+
+    def request_snapshot(self):
+        self._cmd.put(("snapshot", None))
+
+    def set_params(self, params: SimulationParams):
+        self._cmd.put(("params", params))
+
+    def pause(self):
+        self._cmd.put(("pause", None))
+
+    def resume(self):
+        self._cmd.put(("resume", None))

@@ -1,0 +1,116 @@
+"""ctypes binding of include/cfd.h (libcfd_amd.so, built in-tree by
+cfd-demo_amd/Makefile).  No fallback: if the HIP library is missing or cannot
+load, every entry point raises."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(ROOT, "lib", "libcfd_amd.so")
+
+# Every entry point include/cfd.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "cfd_default_params", "cfd_default_grid", "cfd_create", "cfd_rccl_unique_id",
+    "cfd_create_sharded", "cfd_get_slab", "cfd_update", "cfd_update_n", "cfd_piso_step",
+    "cfd_pressure_solve", "cfd_run_phase", "cfd_set_params", "cfd_get_snapshot",
+    "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
+    "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
+    "cfd_last_error", "cfd_abi_version", "cfd_destroy",
+]
+
+
+class CfdGrid(C.Structure):
+    _fields_ = [("nx", C.c_uint64), ("ny", C.c_uint64), ("lx", C.c_float), ("ly", C.c_float),
+                ("has_cylinder", C.c_int32), ("cylinder_x", C.c_float),
+                ("cylinder_y", C.c_float), ("cylinder_radius", C.c_float)]
+
+
+class CfdParams(C.Structure):
+    _fields_ = [("dt", C.c_float), ("viscosity", C.c_float),
+                ("target_inlet_velocity", C.c_float), ("velocity_scheme", C.c_int32),
+                ("inlet_profile", C.c_int32), ("pressure_solver", C.c_int32),
+                ("jacobi_iters", C.c_int32), ("corrector_passes", C.c_int32),
+                ("tol_enabled", C.c_int32), ("p_tol", C.c_float), ("bc_kind", C.c_int32)]
+
+
+class CfdResiduals(C.Structure):
+    _fields_ = [("simulation_step", C.c_uint64), ("simulation_time", C.c_float),
+                ("dt", C.c_float), ("p", C.c_float), ("u", C.c_float), ("v", C.c_float),
+                ("step_time_s", C.c_double), ("piso_substeps", C.c_uint32),
+                ("jacobi_sweeps_total", C.c_uint64)]
+
+
+FP = C.POINTER(C.c_float)
+
+
+class CfdState(C.Structure):
+    _fields_ = [("u", FP), ("v", FP), ("p", FP), ("u_star", FP), ("v_star", FP),
+                ("p_prime", FP), ("rhs", FP), ("dt", C.c_float), ("simulation_time", C.c_float),
+                ("simulation_step", C.c_uint64), ("last_p_residual", C.c_float),
+                ("last_u_residual", C.c_float), ("last_v_residual", C.c_float),
+                ("jacobi_sweeps_total", C.c_uint64)]
+
+
+class CfdError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load libcfd_amd.so; raise (never fall back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"HIP library {LIB_PATH} not built: run `make -C {ROOT}` "
+            "(or __graft_entry__.build()). There is no CPU fallback.")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    sig = {
+        "cfd_default_params": (None, [C.POINTER(CfdParams)]),
+        "cfd_default_grid": (None, [C.POINTER(CfdGrid)]),
+        "cfd_create": (i32, [C.POINTER(CfdGrid), C.POINTER(CfdParams), i32, C.POINTER(vp)]),
+        "cfd_rccl_unique_id": (i32, [C.c_char_p]),
+        "cfd_create_sharded": (i32, [C.POINTER(CfdGrid), C.POINTER(CfdParams), i32, i32, i32,
+                                     C.c_char_p, C.POINTER(vp)]),
+        "cfd_get_slab": (i32, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "cfd_update": (i32, [vp]),
+        "cfd_update_n": (i32, [vp, i32]),
+        "cfd_piso_step": (i32, [vp, f32]),
+        "cfd_pressure_solve": (i32, [vp, FP]),
+        "cfd_run_phase": (i32, [vp, i32, f32]),
+        "cfd_set_params": (i32, [vp, C.POINTER(CfdParams)]),
+        "cfd_get_snapshot": (i32, [vp, FP, FP, FP, FP]),
+        "cfd_get_residuals": (i32, [vp, C.POINTER(CfdResiduals)]),
+        "cfd_get_state": (i32, [vp, C.POINTER(CfdState)]),
+        "cfd_set_state": (i32, [vp, C.POINTER(CfdState)]),
+        "cfd_get_masks": (i32, [vp, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
+        "cfd_synchronize": (i32, [vp]),
+        "cfd_profile_sweeps": (i32, [vp, i32, C.POINTER(C.c_double)]),
+        "cfd_timing_begin": (i32, [vp]),
+        "cfd_timing_end": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+        "cfd_get_halo_depth": (i32, [vp]),
+        "cfd_last_error": (C.c_char_p, []),
+        "cfd_abi_version": (i32, []),
+        "cfd_destroy": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(fn: str, rc: int):
+    if rc != 0:
+        msg = load().cfd_last_error()
+        raise CfdError(fn, rc, msg.decode() if msg else "")

@@ -1,0 +1,93 @@
+// cfd_internal.h — device-side data layout and kernel launch interface of the
+// MI355X pressure-projection path.  Shared by cfd_kernels.hip (device code)
+// and cfd_model.hip (host runtime behind include/cfd.h).
+//
+// Layout in HBM (one slab per GPU; a single-GPU model is the 1-slab case):
+//   every field is row-major with x fastest and the reference's pitches
+//   (u: nx+1, v: nx, p/rhs/p': nx — model.rs:161-214), so the reference's
+//   flat wrap-around reads (U(nx+1,j) == U(0,j+1)) are plain loads here.
+//   "local row" lj = global row j - j0.  Base pointers point at local row 0;
+//   ghost rows sit at negative lj and at lj >= nyl:
+//     u, u_old, u_star : rows [-G, nyl+G)        (G = 2)
+//     v, v_old, v_star : rows [-G, nyl+1+G)      (v row nyl is the face shared
+//                                                 with the rank above)
+//     p, rhs           : rows [0, nyl)
+//     p' (two buffers) : rows [-HG, nyl+HG)      (HG = halo depth >= 1)
+//   mask_u rows [0,nyl), mask_v rows [0,nyl] (u8, same pitches).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfd {
+
+constexpr int kGhostUV = 2;
+constexpr int kMaxSweeps = 4096;   // per pressure solve
+constexpr int kMaxPasses = 64;     // corrector passes + 1
+
+// Device-resident control block: every data-dependent decision of
+// Model::update lives here so a whole step can be enqueued (or replayed as a
+// hipGraph) with no host round trip.
+struct Ctl {
+    float dt;               // Model::dt (model.rs:170)
+    float time;             // simulation_time
+    uint32_t step;          // simulation_step
+    float inlet;            // current_inlet_velocity (set at step start)
+    int32_t cur;            // which p' buffer holds the current p'
+    uint32_t n_exec_last;   // sweeps executed by the last solve
+    float last_p;           // last_pressure_residual
+    float res_u, res_v;     // last_u_residual / last_v_residual
+    uint32_t red[4];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|
+    uint64_t sweeps_total;
+    int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
+    uint32_t err[kMaxSweeps];        // per-sweep max |p'new - p'| as f32 bits
+};
+
+// Scalars every kernel needs; passed by value as a kernel argument.
+struct Geom {
+    int32_t nx, ny;       // global pressure cells
+    int32_t j0, nyl;      // global row of local row 0; owned rows
+    int32_t hg;           // p' halo depth
+    float dx, dy, nu, ly;
+    float target_inlet;
+    int32_t scheme, profile, bc_kind;
+    int32_t tol_enabled;
+    float p_tol;
+    int32_t jacobi_iters;
+};
+
+struct Fields {
+    float *u, *v, *u_old, *v_old, *u_star, *v_star;   // at local row 0
+    float *p, *rhs;
+    float *pp[2];                                      // p' ping-pong
+    const uint8_t *mask_u, *mask_v;
+    const int32_t *obs;       // (i, j_global) pairs, cells touching this slab
+    int32_t n_obs;
+    size_t u_alloc, v_alloc;  // floats in the u/v allocations (incl. ghosts)
+    float *u_alloc_base, *v_alloc_base, *u_old_base, *v_old_base, *u_star_base, *v_star_base;
+    Ctl *ctl;
+};
+
+// ---- launchers (cfd_kernels.hip) ----
+// pass < 0 means "not inside the corrector loop" (always runs).
+void launch_step_begin(const Geom &g, const Fields &f, hipStream_t s);
+void launch_copy_star(const Geom &g, const Fields &f, int pass, hipStream_t s);
+void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
+                       hipStream_t s);
+// One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).
+void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int row_lo,
+                         int row_hi, hipStream_t s);
+void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
+                           hipStream_t s);
+void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
+                      hipStream_t s);
+void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);
+void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s);
+void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
+
+// Jacobi kernel geometry (exported for the roofline bookkeeping in bench).
+constexpr int kJacRowsPerWave = 16;
+constexpr int kJacWavesPerBlock = 4;
+
+}  // namespace cfd

@@ -1,0 +1,674 @@
+// cfd_kernels.hip — CDNA4 (gfx950) kernels for cfd-demo's Model::update hot path.
+//
+// Every kernel reproduces the reference's f32 arithmetic bit for bit: the
+// file is compiled with -ffp-contract=off (Rust never fuses a*b+c), `/` is
+// HIP's default correctly-rounded f32 division, denormals are kept, and each
+// expression keeps the reference's evaluation order.  Maxima are exact and
+// order-independent, so the reductions (wave shuffles + one atomicMax on the
+// f32 bit pattern of a non-negative value) are deterministic.
+//
+// Citations are /root/reference/src/model.rs line numbers.
+#include "cfd_internal.h"
+
+namespace cfd {
+
+namespace {
+
+constexpr int kBlock = 256;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float dt_of(const Ctl *c, float dt_override) {
+    return __builtin_isnan(dt_override) ? c->dt : dt_override;
+}
+
+__device__ __forceinline__ bool pass_off(const Ctl *c, int pass) {
+    return pass >= 0 && c->go[pass] == 0;
+}
+
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    return m;
+}
+
+// ------------------------------------------------------------- copies (K0/K5b)
+
+__device__ __forceinline__ void copy4(float *__restrict__ dst, const float *__restrict__ src,
+                                      size_t n4, size_t tid, size_t stride) {
+    const float4 *s = reinterpret_cast<const float4 *>(src);
+    float4 *d = reinterpret_cast<float4 *>(dst);
+    for (size_t k = tid; k < n4; k += stride) d[k] = s[k];
+}
+
+// update() prologue (model.rs:307-316): u_old <- u, v_old <- v, inlet ramp.
+__global__ __launch_bounds__(kBlock) void k_step_begin(Geom g, Fields f) {
+    const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    copy4(f.u_old_base, f.u_alloc_base, f.u_alloc / 4, tid, stride);
+    copy4(f.v_old_base, f.v_alloc_base, f.v_alloc / 4, tid, stride);
+    if (tid == 0) {
+        Ctl *c = f.ctl;
+        const uint32_t st = c->step;
+        // (simulation_step as f32 / ramp_up_steps as f32) * target (model.rs:311-316)
+        c->inlet = st < 100u ? ((float)st / 100.0f) * g.target_inlet : g.target_inlet;
+        c->go[0] = 1;
+    }
+}
+
+// u_star <- u, v_star <- v before each extra correction pass (model.rs:698-699).
+__global__ __launch_bounds__(kBlock) void k_copy_star(Fields f, int pass) {
+    if (pass_off(f.ctl, pass)) return;
+    const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    copy4(f.u_star_base, f.u_alloc_base, f.u_alloc / 4, tid, stride);
+    copy4(f.v_star_base, f.v_alloc_base, f.v_alloc / 4, tid, stride);
+}
+
+// ---------------------------------------------------------- u predictor (K1)
+
+// u* on global rows 1..=ny-2, faces 1..=nx (model.rs:538-580 + compute_ustar
+// :382-436).  One thread per face; neighbour reuse comes from L1/L2.  Flux
+// velocities are the raw v values (get_v_north/south :1056-1069).
+template <int SCHEME>
+__global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float dt_override,
+                                                        int row_lo, int nbx) {
+    const int i = 1 + (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + (int)(blockIdx.x / nbx);
+    const int nx = g.nx, ny = g.ny, W = nx + 1;
+    if (i > nx) return;
+    const int j = g.j0 + lj;
+    const float *__restrict__ u = f.u;
+    const float *__restrict__ v = f.v;
+    const long c = (long)lj * W + i;
+    const long cv = (long)lj * nx + i;
+    const float uc = u[c], ue1 = u[c + 1], uw1 = u[c - 1], un1 = u[c + W], us1 = u[c - W];
+    const float vn = v[cv + nx], vs = v[cv];
+    float ue, uw, un, us;
+    if (SCHEME == 0) {
+        // u_face_{e,w,n,s}_first_order (:893-908, :929-941, :966-981, :1011-1026)
+        ue = ((uc + ue1) * 0.5f >= 0.0f) ? uc : ue1;
+        uw = ((uw1 + uc) * 0.5f >= 0.0f) ? uw1 : uc;
+        un = (vn >= 0.0f) ? uc : un1;
+        us = (vs >= 0.0f) ? us1 : uc;
+    } else {
+        const size_t ulen = (size_t)W * (size_t)ny;
+        // u_face_e_second_order (:911-926)
+        if (uc >= 0.0f) {
+            ue = (i > 1) ? 1.5f * uc - 0.5f * u[c - 1] : uc;
+        } else if (((size_t)(i + 1) + (size_t)j * W) + 1 < ulen && i < nx - 1) {
+            ue = 1.5f * ue1 - 0.5f * u[c + 2];
+        } else {
+            ue = ue1;
+        }
+        // u_face_w_second_order (:944-963)
+        if (uw1 >= 0.0f) {
+            uw = (i > 2) ? 1.5f * uw1 - 0.5f * u[c - 2] : uw1;
+        } else {
+            uw = (i < nx) ? 1.5f * uc - 0.5f * ue1 : uc;
+        }
+        // u_face_n_second_order (:992-1008), decision on averaged v (:983-989)
+        const float vnb = 0.5f * (v[cv + nx - 1] + v[cv + nx]);
+        if (vnb >= 0.0f) {
+            un = (j > 1) ? 1.5f * uc - 0.5f * us1 : uc;
+        } else if ((size_t)i + (size_t)(j + 2) * W < ulen && j < ny - 1) {
+            un = 1.5f * un1 - 0.5f * u[c + 2 * W];
+        } else {
+            un = un1;
+        }
+        // u_face_s_second_order (:1037-1053), decision on averaged v (:1028-1034)
+        const float vsb = 0.5f * (v[cv - 1] + v[cv]);
+        if (vsb >= 0.0f) {
+            us = (j > 1) ? 1.5f * us1 - 0.5f * u[c - 2 * W] : us1;
+        } else if (j < ny) {
+            us = 1.5f * uc - 0.5f * un1;
+        } else {
+            us = uc;
+        }
+    }
+    const float dx = g.dx, dy = g.dy, nu = g.nu;
+    const float dt = dt_of(f.ctl, dt_override);
+    const float f_e = ue * ue;
+    const float f_w = uw * uw;
+    const float f_n = vn * un;
+    const float f_s = vs * us;
+    const float convective = (f_e - f_w) / dx + (f_n - f_s) / dy;
+    const float laplace = (ue1 - 2.0f * uc + uw1) / (dx * dx) + (un1 - 2.0f * uc + us1) / (dy * dy);
+    float r = uc + dt * (-convective + nu * laplace);
+    if (f.mask_u[(long)lj * W + i] == 1) r = 0.0f;
+    f.u_star[c] = r;
+}
+
+// ---------------------------------------------------------- v predictor (K2)
+
+// v* on global rows 1..=ny-1, columns 1..=nx-1 (model.rs:586-670 +
+// compute_vstar :439-521).  Advecting u is the raw face value U(i+1,j),
+// U(i,j).  SecondOrder: the lane of column nx-1 is never filled (:647-650),
+// so all six inputs are 0.0 there.
+template <int SCHEME>
+__global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float dt_override,
+                                                        int row_lo, int nbx) {
+    const int i = 1 + (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + (int)(blockIdx.x / nbx);
+    const int nx = g.nx, ny = g.ny, W = nx + 1;
+    if (i > nx - 1) return;
+    const int j = g.j0 + lj;
+    const float *__restrict__ u = f.u;
+    const float *__restrict__ v = f.v;
+    const long cv = (long)lj * nx + i;
+    const long cu = (long)lj * W + i;
+    const float vc = v[cv], ve1 = v[cv + 1], vw1 = v[cv - 1], vn1 = v[cv + nx], vs1 = v[cv - nx];
+    float uE = u[cu + 1], uW = u[cu];
+    float ve, vw, vn, vs;
+    if (SCHEME == 0) {
+        // v_face_{e,w,n,s}_first_order(_scalar) (:1073-1095, :1116-1142, :1163-1185, :1207-1229)
+        ve = (uE >= 0.0f) ? vc : ve1;
+        vw = (uW >= 0.0f) ? vw1 : vc;
+        vn = (0.5f * (vc + vn1) >= 0.0f) ? vc : vn1;
+        vs = (0.5f * (vs1 + vc) >= 0.0f) ? vs1 : vc;
+    } else if (i >= nx - 1) {
+        uE = 0.0f;
+        uW = 0.0f;
+        ve = vw = vn = vs = 0.0f;
+    } else {
+        const size_t vlen = (size_t)nx * (size_t)(ny + 1);
+        const size_t idx = (size_t)i + (size_t)j * nx;
+        // v_face_e_second_order (:1098-1113)
+        if (uE >= 0.0f) {
+            ve = (i > 0) ? 1.5f * vc - 0.5f * vw1 : vc;
+        } else if (idx + 2 < vlen && i < nx - 2) {
+            ve = 1.5f * ve1 - 0.5f * v[cv + 2];
+        } else {
+            ve = ve1;
+        }
+        // v_face_w_second_order (:1145-1160)
+        if (uW >= 0.0f) {
+            vw = (i > 1) ? 1.5f * vw1 - 0.5f * v[cv - 2] : vw1;
+        } else {
+            vw = (i < nx - 1) ? 1.5f * vc - 0.5f * ve1 : vc;
+        }
+        // v_face_n_second_order (:1188-1204)
+        if (0.5f * (vc + vn1) >= 0.0f) {
+            vn = (j > 1) ? 1.5f * vc - 0.5f * vs1 : vc;
+        } else if ((size_t)i + (size_t)(j + 2) * nx < vlen && j < ny - 1) {
+            vn = 1.5f * vn1 - 0.5f * v[cv + 2 * nx];
+        } else {
+            vn = vn1;
+        }
+        // v_face_s_second_order (:1232-1248)
+        if (0.5f * (vs1 + vc) >= 0.0f) {
+            vs = (j > 1) ? 1.5f * vs1 - 0.5f * v[cv - 2 * nx] : vs1;
+        } else if (j < ny) {
+            vs = 1.5f * vc - 0.5f * vn1;
+        } else {
+            vs = vc;
+        }
+    }
+    float r;
+    if (f.mask_v[cv] == 1) {
+        r = 0.0f;
+    } else {
+        const float dx = g.dx, dy = g.dy, nu = g.nu;
+        const float dt = dt_of(f.ctl, dt_override);
+        const float f_e = uE * ve;
+        const float f_w = uW * vw;
+        const float f_n = vn * vn;
+        const float f_s = vs * vs;
+        const float convective = (f_e - f_w) / dx + (f_n - f_s) / dy;
+        const float laplace =
+            (ve1 - 2.0f * vc + vw1) / (dx * dx) + (vn1 - 2.0f * vc + vs1) / (dy * dy);
+        r = vc + dt * (-convective + nu * laplace);
+    }
+    f.v_star[cv] = r;
+}
+
+// ------------------------------------------------------------ divergence (K3)
+
+// rhs = div(u*, v*) / dt on every owned pressure cell (model.rs:1406-1440).
+__global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pass,
+                                                       float dt_override, int nbx) {
+    if (pass_off(f.ctl, pass)) return;
+    const int i = (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = (int)(blockIdx.x / nbx);
+    const int nx = g.nx, W = nx + 1;
+    if (i >= nx) return;
+    const float dt = dt_of(f.ctl, dt_override);
+    const float *__restrict__ us = f.u_star;
+    const float *__restrict__ vs = f.v_star;
+    const float u_e = us[(long)lj * W + i + 1];
+    const float u_w = us[(long)lj * W + i];
+    const float v_n = vs[(long)(lj + 1) * nx + i];
+    const float v_s = vs[(long)lj * nx + i];
+    f.rhs[(long)lj * nx + i] = ((u_e - u_w) / g.dx + (v_n - v_s) / g.dy) / dt;
+}
+
+// ---------------------------------------------------------------- Jacobi (K4)
+
+// One weighted-Jacobi sweep (omega 0.75) with the p' boundary conditions
+// fused into the stores (model.rs:748-815).
+//
+// Mapping: a wave owns 64 float4 column chunks (256 columns) of one row
+// segment of R rows and marches up the segment, keeping rows j-1, j, j+1 in
+// registers: p' and rhs are each read from HBM once per sweep, p'_new written
+// once (12 B per cell-update), and horizontal neighbours come from adjacent
+// lanes (__shfl) instead of re-reads.  Rows are processed 4 at a time with all
+// 8 row loads of a group issued before any arithmetic.
+//
+// Boundary conditions, as stores (model.rs:807-815 applied after the swap):
+// the reference's final values are P(0,j) = N(1,j), P(nx-1,j) = 0,
+// P(i,0) = N(i,1), P(i,ny-1) = N(i,ny-2) for the freshly computed interior
+// N — so column 0 takes column 1's value, column nx-1 stores 0, and the
+// threads computing global rows 1 and ny-2 also store rows 0 and ny-1.
+// Column nx-1's own update (which reads the wrapped P(0,j+1), Q5) is never
+// stored, exactly as the reference overwrites it.
+//
+// Residual: max |N - P| over columns 1..=nx-8 only (the reference's full
+// 8-lane chunks; the scalar tail :755-772 never updates max_error), owned
+// rows only, NaN-ignoring like reduce_max.  One atomicMax per wave.
+template <int R>
+__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, int pass, int it, int row_lo, int row_hi, int nbx) {
+    if (pass_off(ctl, pass)) return;
+    // early exit of the previous sweep (model.rs:816): a skipped sweep leaves
+    // its err slot at 0 so every later sweep of the solve skips too.
+    if (g.tol_enabled && it > 0 && __uint_as_float(ctl->err[it - 1]) < g.p_tol) return;
+
+    const int nx = g.nx, nch = nx >> 2, hg = g.hg, nyl = g.nyl;
+    const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int bx = (int)blockIdx.x % nbx, seg = (int)blockIdx.x / nbx;
+    const int wcol = bx * kJacWavesPerBlock + wave;
+    if (wcol * 64 >= nch) return;                         // wave-uniform
+    const int ch = wcol * 64 + lane;
+    const bool valid = ch < nch;
+    const int r0 = row_lo + seg * R;
+    const int r1 = min(r0 + R, row_hi);
+    if (r0 >= r1) return;
+
+    // pa/pb: the two p' allocations (first ghost row); (cur + it) picks the
+    // source.  Loads go through buffer descriptors: a lane with nothing to
+    // load gets an out-of-range offset and reads 0 without a branch.
+    const int si = (ctl->cur + it) & 1;
+    float *src_alloc = si ? pb : pa;
+    float *dst_alloc = si ? pa : pb;
+    const int pbytes = (nyl + 2 * hg) * nx * 4;
+    const __amdgpu_buffer_rsrc_t rs_p =
+        __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_r =
+        __builtin_amdgcn_make_buffer_rsrc((void *)rhs, 0, nyl * nx * 4, 0x00020000);
+    float *__restrict__ dst = dst_alloc + (long)hg * nx;
+
+    const float dx = g.dx, dy = g.dy;
+    const float dx_sq = dx * dx;
+    const float dy_sq = dy * dy;
+    const float omega = 0.75f;
+    const float om1 = 1.0f - omega;
+    const float denom = 2.0f / (dx * dx) + 2.0f / (dy * dy);
+
+    constexpr int kOOB = -16;   // >= num_records as unsigned: reads 0
+    const int col = 4 * ch;
+    const int row_bytes = nx * 4;
+    // byte offsets at local row 0 (p' offsets include the hg ghost rows)
+    const int off_p = valid ? (hg * nx + col) * 4 : kOOB;
+    const int off_r = valid ? col * 4 : kOOB;
+    const int off_l = (lane == 0 && ch > 0 && valid) ? (hg * nx + col - 1) * 4 : kOOB;
+    const int off_rt = (lane == 63 && ch + 1 < nch) ? (hg * nx + col + 4) * 4 : kOOB;
+    const bool e0 = (col >= 1) && (col <= nx - 8);   // residual columns 1..=nx-8
+    const bool e1 = (col + 1 <= nx - 8);
+    const bool e2 = (col + 2 <= nx - 8);
+    const bool e3 = (col + 3 <= nx - 8);
+    const int gj_first = 1 - g.j0, gj_last = g.ny - 2 - g.j0;   // local rows of global 1, ny-2
+
+    auto ld4 = [&](const __amdgpu_buffer_rsrc_t &rs, int off, int row) -> float4 {
+        const int o = off < 0 ? off : off + row * row_bytes;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                           __uint_as_float(v.w));
+    };
+    auto ld1 = [&](int off, int row) -> float {
+        const int o = off < 0 ? off : off + row * row_bytes;
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_p, o, 0, 0));
+    };
+
+    float m = 0.0f;
+    // sliding window: w0..w5 = p' rows j-1 .. j+4 of the current 4-row group;
+    // rows past r1 are clamped to r1 (always inside the allocation, unused)
+    float4 w0 = ld4(rs_p, off_p, r0 - 1);
+    float4 w1 = ld4(rs_p, off_p, r0);
+    for (int j = r0; j < r1; j += 4) {
+        const bool l1 = j + 1 < r1, l2 = j + 2 < r1, l3 = j + 3 < r1;
+        const int j1c = l1 ? j + 1 : j, j2c = l2 ? j + 2 : j, j3c = l3 ? j + 3 : j;
+        // issue every load of the group before any arithmetic
+        const float4 w2 = ld4(rs_p, off_p, j + 1);
+        const float4 w3 = ld4(rs_p, off_p, j1c + 1);
+        const float4 w4 = ld4(rs_p, off_p, j2c + 1);
+        const float4 w5 = ld4(rs_p, off_p, j3c + 1);
+        const float4 h0 = ld4(rs_r, off_r, j);
+        const float4 h1 = ld4(rs_r, off_r, j1c);
+        const float4 h2 = ld4(rs_r, off_r, j2c);
+        const float4 h3 = ld4(rs_r, off_r, j3c);
+        const float lf0 = ld1(off_l, j), lf1 = ld1(off_l, j1c), lf2 = ld1(off_l, j2c),
+                    lf3 = ld1(off_l, j3c);
+        const float rt0 = ld1(off_rt, j), rt1 = ld1(off_rt, j1c), rt2 = ld1(off_rt, j2c),
+                    rt3 = ld1(off_rt, j3c);
+
+        auto row_update = [&](int row, const float4 &B, const float4 &C, const float4 &T,
+                              const float4 &Rh, float lf, float rt) {
+            const float horiz_l = __shfl_up(C.w, 1, 64);
+            const float horiz_r = __shfl_down(C.x, 1, 64);
+            const float L0 = (lane == 0) ? lf : horiz_l;
+            const float R3 = (lane == 63) ? rt : horiz_r;
+            const float cc[4] = {C.x, C.y, C.z, C.w};
+            const float rr[4] = {C.y, C.z, C.w, R3};
+            const float ll[4] = {L0, C.x, C.y, C.z};
+            const float tt[4] = {T.x, T.y, T.z, T.w};
+            const float bb[4] = {B.x, B.y, B.z, B.w};
+            const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
+            float n[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float horizontal = (rr[k] + ll[k]) / dx_sq;
+                const float vertical = (tt[k] + bb[k]) / dy_sq;
+                const float p_update = (horizontal + vertical - hh[k]) / denom;
+                n[k] = omega * p_update + om1 * cc[k];
+            }
+            if (row >= 0 && row < nyl) {
+                if (e0) m = fmaxf(m, fabsf(n[0] - cc[0]));
+                if (e1) m = fmaxf(m, fabsf(n[1] - cc[1]));
+                if (e2) m = fmaxf(m, fabsf(n[2] - cc[2]));
+                if (e3) m = fmaxf(m, fabsf(n[3] - cc[3]));
+            }
+            float4 o = make_float4(n[0], n[1], n[2], n[3]);
+            if (ch == 0) o.x = n[1];          // P(0,j) = P(1,j)
+            if (ch == nch - 1) o.w = 0.0f;    // P(nx-1,j) = 0
+            if (valid) {
+                *reinterpret_cast<float4 *>(dst + (long)row * nx + col) = o;
+                if (row == gj_first)          // P(i,0) = P(i,1)
+                    *reinterpret_cast<float4 *>(dst + (long)(row - 1) * nx + col) = o;
+                if (row == gj_last)           // P(i,ny-1) = P(i,ny-2)
+                    *reinterpret_cast<float4 *>(dst + (long)(row + 1) * nx + col) = o;
+            }
+        };
+        row_update(j, w0, w1, w2, h0, lf0, rt0);
+        if (l1) row_update(j + 1, w1, w2, w3, h1, lf1, rt1);
+        if (l2) row_update(j + 2, w2, w3, w4, h2, lf2, rt2);
+        if (l3) row_update(j + 3, w3, w4, w5, h3, lf3, rt3);
+        w0 = w4;
+        w1 = w5;
+    }
+    m = wave_max(m);
+    if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it], __float_as_uint(m));
+}
+
+// End of a pressure solve: how many sweeps ran, which buffer is current, the
+// returned residual (model.rs:816-823), and whether the corrector loop goes on
+// (model.rs:721-723).  Resets the per-sweep slots for the next solve.
+__global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
+                                                           int check_break) {
+    Ctl *c = f.ctl;
+    __shared__ int go_s;
+    if (threadIdx.x == 0) {
+        const int go = pass < 0 ? 1 : c->go[pass];
+        if (go) {
+            int n = iters;
+            if (g.tol_enabled && iters > 0) {
+                n = 1;
+                while (n < iters && __uint_as_float(c->err[n - 1]) >= g.p_tol) ++n;
+            }
+            const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
+            c->cur = (c->cur + n) & 1;
+            c->last_p = res;
+            c->n_exec_last = (uint32_t)n;
+            c->sweeps_total += (uint64_t)n;
+        }
+        if (pass >= 0 && pass + 1 <= kMaxPasses)
+            c->go[pass + 1] = (go && !(check_break && g.tol_enabled && c->last_p < g.p_tol)) ? 1 : 0;
+        go_s = go;
+    }
+    __syncthreads();
+    if (go_s)
+        for (int k = threadIdx.x; k < iters; k += blockDim.x) c->err[k] = 0u;
+}
+
+// ------------------------------------------------------------- corrector (K5)
+
+// apply_corrector (model.rs:1334-1404).  u: all owned rows, faces 1..nx-1;
+// faces nx-7..nx-1 are the scalar tail and associate (dt * dp) / dx (Q9).
+// v: global rows 1..=ny-1 held by this slab (incl. the shared face row).
+// p += p'.
+__global__ __launch_bounds__(kBlock) void k_corrector(Geom g, Fields f, int pass,
+                                                      float dt_override, int nbx) {
+    Ctl *c = f.ctl;
+    if (pass_off(c, pass)) return;
+    const int i = (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
+    const int lj = (int)(blockIdx.x / nbx);                             // 0..nyl
+    const int nx = g.nx, W = nx + 1;
+    if (i > nx) return;
+    const float dt = dt_of(c, dt_override);
+    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+    const int j = g.j0 + lj;
+    if (lj < g.nyl && i >= 1 && i <= nx - 1) {
+        const float p_right = pp[(long)lj * nx + i];
+        const float p_left = pp[(long)lj * nx + i - 1];
+        const long k = (long)lj * W + i;
+        if (i >= nx - 7)
+            f.u[k] = f.u_star[k] - dt * (p_right - p_left) / g.dx;
+        else
+            f.u[k] = f.u_star[k] - dt * ((p_right - p_left) / g.dx);
+    }
+    if (i < nx && j >= 1 && j <= g.ny - 1) {
+        const float p_top = pp[(long)lj * nx + i];
+        const float p_bottom = pp[(long)(lj - 1) * nx + i];
+        const long k = (long)lj * nx + i;
+        f.v[k] = f.v_star[k] - dt * ((p_top - p_bottom) / g.dy);
+    }
+    if (i < nx && lj < g.nyl) {
+        const long k = (long)lj * nx + i;
+        f.p[k] = f.p[k] + pp[k];
+    }
+}
+
+// ------------------------------------------------- velocity boundaries (K6)
+
+// apply_boundary_conditions (model.rs:826-875), in the reference's order; a
+// single workgroup with barriers between the phases that touch the same
+// faces.  bc_kind 1 = build-defined lid-driven cavity.
+__global__ __launch_bounds__(1024) void k_boundary(Geom g, Fields f) {
+    const int nx = g.nx, W = nx + 1, nyl = g.nyl;
+    const float inlet = f.ctl->inlet;
+    float *__restrict__ u = f.u;
+    float *__restrict__ v = f.v;
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int lj = t; lj < nyl; lj += nt) {
+        const int j = g.j0 + lj;
+        if (g.bc_kind == 0) {
+            float val;
+            if (g.profile == 0) {
+                val = inlet;
+            } else {
+                const float y = ((float)j + 0.5f) * g.dy;
+                const float center = g.ly / 2.0f;
+                const float radius = g.ly / 2.0f;
+                const float q = (y - center) / radius;
+                const float pv = inlet * (1.0f - q * q);
+                val = pv < 0.0f ? 0.0f : pv;
+            }
+            u[(long)lj * W] = val;
+            u[(long)lj * W + nx] = u[(long)lj * W + nx - 1];
+        } else {
+            u[(long)lj * W] = 0.0f;
+            u[(long)lj * W + nx] = 0.0f;
+        }
+    }
+    __syncthreads();
+    const bool has_bottom = g.j0 == 0;
+    const bool has_top = g.j0 + nyl == g.ny;
+    for (int i = t; i <= nx; i += nt) {
+        if (has_bottom) u[i] = 0.0f;
+        if (has_top) {
+            const float lid = (g.bc_kind == 1 && i > 0 && i < nx) ? inlet : 0.0f;
+            u[(long)(nyl - 1) * W + i] = lid;
+        }
+    }
+    for (int i = t; i < nx; i += nt) {
+        if (has_bottom) v[i] = 0.0f;
+        if (has_top) v[(long)nyl * nx + i] = 0.0f;
+    }
+    __syncthreads();
+    for (int k = t; k < f.n_obs; k += nt) {
+        const int oi = f.obs[2 * k], oj = f.obs[2 * k + 1];
+        const int lj = oj - g.j0;
+        if (lj >= 0 && lj < nyl) u[(long)lj * W + oi] = 0.0f;
+        if (lj >= 0 && lj <= nyl) v[(long)lj * nx + oi] = 0.0f;
+    }
+}
+
+// ------------------------------------------------- step reductions (K7)
+
+// max |u - u_old|, max |v - v_old| (model.rs:333-344) and max |u|, max |v|
+// (compute_automatic_time_step :879-880) over the owned rows; f32::max
+// ignores NaN, as fmaxf does.
+__global__ __launch_bounds__(kBlock) void k_step_reduce(Geom g, Fields f) {
+    const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t nu = (size_t)g.nyl * (g.nx + 1), nv = (size_t)(g.nyl + 1) * g.nx;
+    float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
+    for (size_t k = tid; k < nu; k += stride) {
+        const float a = f.u[k];
+        du = fmaxf(du, fabsf(a - f.u_old[k]));
+        mu = fmaxf(mu, fabsf(a));
+    }
+    for (size_t k = tid; k < nv; k += stride) {
+        const float a = f.v[k];
+        dv = fmaxf(dv, fabsf(a - f.v_old[k]));
+        mv = fmaxf(mv, fabsf(a));
+    }
+    du = wave_max(du);
+    dv = wave_max(dv);
+    mu = wave_max(mu);
+    mv = wave_max(mv);
+    if ((threadIdx.x & 63) == 0) {
+        uint32_t *r = f.ctl->red;
+        if (du > 0.f) atomicMax(&r[0], __float_as_uint(du));
+        if (dv > 0.f) atomicMax(&r[1], __float_as_uint(dv));
+        if (mu > 0.f) atomicMax(&r[2], __float_as_uint(mu));
+        if (mv > 0.f) atomicMax(&r[3], __float_as_uint(mv));
+    }
+}
+
+// update() epilogue (model.rs:347-377): residuals, step/time, CFL dt.
+__global__ void k_step_finalize(Geom g, Fields f) {
+    if (threadIdx.x != 0) return;
+    Ctl *c = f.ctl;
+    c->res_u = __uint_as_float(c->red[0]);
+    c->res_v = __uint_as_float(c->red[1]);
+    const float max_vel = fmaxf(__uint_as_float(c->red[2]), __uint_as_float(c->red[3]));
+    c->step += 1u;
+    c->time = c->time + c->dt;
+    const float previous_dt = c->dt;
+    float new_dt;
+    if (max_vel == 0.0f) {
+        new_dt = c->dt;
+    } else {
+        const float cfl = 0.2f;
+        const float dt_cfl = cfl * fminf(g.dx, g.dy) / max_vel;
+        new_dt = fminf(dt_cfl, c->dt);
+    }
+    c->dt = (new_dt > previous_dt) ? fminf(new_dt, previous_dt * 1.1f) : new_dt;
+    c->red[0] = c->red[1] = c->red[2] = c->red[3] = 0u;
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+inline int copy_grid(size_t n4) {
+    long b = cdiv((long)n4, kBlock);
+    return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+
+void launch_step_begin(const Geom &g, const Fields &f, hipStream_t s) {
+    size_t n4 = f.u_alloc > f.v_alloc ? f.u_alloc / 4 : f.v_alloc / 4;
+    hipLaunchKernelGGL(k_step_begin, dim3(copy_grid(n4)), dim3(kBlock), 0, s, g, f);
+}
+
+void launch_copy_star(const Geom &g, const Fields &f, int pass, hipStream_t s) {
+    size_t n4 = f.u_alloc > f.v_alloc ? f.u_alloc / 4 : f.v_alloc / 4;
+    hipLaunchKernelGGL(k_copy_star, dim3(copy_grid(n4)), dim3(kBlock), 0, s, f, pass);
+}
+
+void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+    const int glo = g.j0 > 1 ? g.j0 : 1;
+    const int ghi = (g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2);
+    if (ghi < glo) return;
+    const int nbx = cdiv(g.nx, kBlock);
+    const dim3 grid(nbx * (ghi - glo + 1));
+    if (g.scheme == 0)
+        hipLaunchKernelGGL(k_u_predictor<0>, grid, dim3(kBlock), 0, s, g, f, dt_override,
+                           glo - g.j0, nbx);
+    else
+        hipLaunchKernelGGL(k_u_predictor<1>, grid, dim3(kBlock), 0, s, g, f, dt_override,
+                           glo - g.j0, nbx);
+}
+
+void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+    const int glo = g.j0 > 1 ? g.j0 : 1;
+    const int ghi = (g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1);
+    if (ghi < glo) return;
+    const int nbx = cdiv(g.nx - 1, kBlock);
+    const dim3 grid(nbx * (ghi - glo + 1));
+    if (g.scheme == 0)
+        hipLaunchKernelGGL(k_v_predictor<0>, grid, dim3(kBlock), 0, s, g, f, dt_override,
+                           glo - g.j0, nbx);
+    else
+        hipLaunchKernelGGL(k_v_predictor<1>, grid, dim3(kBlock), 0, s, g, f, dt_override,
+                           glo - g.j0, nbx);
+}
+
+void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
+                       hipStream_t s) {
+    const int nbx = cdiv(g.nx, kBlock);
+    hipLaunchKernelGGL(k_divergence, dim3(nbx * g.nyl), dim3(kBlock), 0, s, g, f, pass,
+                       dt_override, nbx);
+}
+
+void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int row_lo,
+                         int row_hi, hipStream_t s) {
+    if (row_hi <= row_lo) return;
+    const int nch = g.nx / 4;
+    const int nwc = cdiv(nch, 64);
+    const int nbx = cdiv(nwc, kJacWavesPerBlock);
+    const int nseg = cdiv(row_hi - row_lo, kJacRowsPerWave);
+    hipLaunchKernelGGL(k_jacobi<kJacRowsPerWave>, dim3(nbx * nseg),
+                       dim3(kJacWavesPerBlock * 64), 0, s, g, f.pp[0] - (long)g.hg * g.nx,
+                       f.pp[1] - (long)g.hg * g.nx, f.rhs, f.ctl, pass, it, row_lo, row_hi, nbx);
+}
+
+void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize_solve, dim3(1), dim3(kBlock), 0, s, g, f, pass, iters,
+                       check_break);
+}
+
+void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
+                      hipStream_t s) {
+    const int nbx = cdiv(g.nx + 1, kBlock);
+    hipLaunchKernelGGL(k_corrector, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,
+                       dt_override, nbx);
+}
+
+void launch_boundary(const Geom &g, const Fields &f, hipStream_t s) {
+    hipLaunchKernelGGL(k_boundary, dim3(1), dim3(1024), 0, s, g, f);
+}
+
+void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s) {
+    const size_t n = (size_t)(g.nyl + 1) * (g.nx + 1);
+    hipLaunchKernelGGL(k_step_reduce, dim3(copy_grid(n / 4 + 1)), dim3(kBlock), 0, s, g, f);
+}
+
+void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s) {
+    hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(64), 0, s, g, f);
+}
+
+}  // namespace cfd

@@ -1,0 +1,836 @@
+// cfd_model.hip — host runtime behind include/cfd.h.
+//
+// One cfd_model owns one slab of the grid on one GPU: its HBM fields, a HIP
+// stream, the device control block (cfd::Ctl) and, for sharded models, an RCCL
+// communicator with the two neighbouring ranks.  Model::update
+// (/root/reference/src/model.rs:304-379) becomes a fixed sequence of kernel
+// launches on that stream; the data-dependent control flow of the reference
+// (Jacobi early exit :816, corrector-loop break :721, CFL dt :368-377) is
+// decided on the device from Ctl, so a step is enqueued without any host
+// round trip.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/cfd.h"
+#include "cfd_internal.h"
+
+using namespace cfd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(CFD_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+#define RCCL_TRY(expr)                                                                     \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess)                                                             \
+            return fail(CFD_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));    \
+    } while (0)
+
+const float kNaN = std::nanf("");
+
+size_t round4(size_t n) { return (n + 3) & ~size_t(3); }
+
+// Rows [j0, j1) of rank `rank` in an even 1D row-slab split of ny rows.
+void slab_rows(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1) {
+    const uint64_t base = ny / (uint64_t)n_ranks, rem = ny % (uint64_t)n_ranks;
+    const uint64_t r = (uint64_t)rank;
+    *j0 = r * base + (r < rem ? r : rem);
+    *j1 = *j0 + base + (r < rem ? 1 : 0);
+}
+
+}  // namespace
+
+struct cfd_model {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    cfd_grid grid{};
+    cfd_params params{};
+    Geom g{};
+    Fields f{};
+    // allocations
+    float *u_all = nullptr, *v_all = nullptr, *uo_all = nullptr, *vo_all = nullptr;
+    float *us_all = nullptr, *vs_all = nullptr;
+    float *p = nullptr, *rhs = nullptr, *pp_all[2] = {nullptr, nullptr};
+    uint8_t *mask_u = nullptr, *mask_v = nullptr;
+    int32_t *obs = nullptr;
+    Ctl *ctl = nullptr;
+    std::vector<uint8_t> h_mask_u, h_mask_v;
+    // sharding
+    int n_ranks = 1, rank = 0;
+    uint64_t j0 = 0, j1 = 0;
+    ncclComm_t comm = nullptr;
+    int host_cur = 0;   // mirror of ctl->cur, valid when the tolerance is off
+    // timing
+    hipEvent_t ev_step0 = nullptr, ev_step1 = nullptr, ev_prof0 = nullptr, ev_prof1 = nullptr;
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> solve_events;
+    size_t ev_next = 0;
+    uint64_t timed_sweeps = 0, timed_steps = 0;
+    double timed_step_ms = 0.0;
+    bool stepped = false;
+
+    bool sharded() const { return n_ranks > 1; }
+    size_t u_rows_alloc() const { return (size_t)g.nyl + 2 * kGhostUV; }
+    size_t v_rows_alloc() const { return (size_t)g.nyl + 1 + 2 * kGhostUV; }
+
+    hipEvent_t take_event() {
+        if (ev_next == ev_pool.size()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            ev_pool.push_back(e);
+        }
+        return ev_pool[ev_next++];
+    }
+
+    // ---------------------------------------------------------------- halos
+    // u/v ghost rows before the predictors: 2 rows of u and
+    // v each way.  v row nyl is the face shared with the rank above and is
+    // computed redundantly by both ranks, so it is not exchanged.
+    int exchange_uv() {
+        if (!sharded()) return 0;
+        const size_t W = (size_t)g.nx + 1, nx = (size_t)g.nx;
+        const int nyl = g.nyl;
+        RCCL_TRY(ncclGroupStart());
+        if (rank > 0) {
+            const int lo = rank - 1;
+            RCCL_TRY(ncclSend(f.u, 2 * W, ncclFloat, lo, comm, stream));
+            RCCL_TRY(ncclSend(f.v + nx, 2 * nx, ncclFloat, lo, comm, stream));
+            RCCL_TRY(ncclRecv(f.u - 2 * W, 2 * W, ncclFloat, lo, comm, stream));
+            RCCL_TRY(ncclRecv(f.v - 2 * nx, 2 * nx, ncclFloat, lo, comm, stream));
+        }
+        if (rank + 1 < n_ranks) {
+            const int hi = rank + 1;
+            RCCL_TRY(ncclSend(f.u + (size_t)(nyl - 2) * W, 2 * W, ncclFloat, hi, comm, stream));
+            RCCL_TRY(ncclSend(f.v + (size_t)(nyl - 2) * nx, 2 * nx, ncclFloat, hi, comm, stream));
+            RCCL_TRY(ncclRecv(f.u + (size_t)nyl * W, 2 * W, ncclFloat, hi, comm, stream));
+            RCCL_TRY(ncclRecv(f.v + (size_t)(nyl + 1) * nx, 2 * nx, ncclFloat, hi, comm, stream));
+        }
+        RCCL_TRY(ncclGroupEnd());
+        return 0;
+    }
+
+    // p' halo: `rows` owned boundary rows of buffer `buf` each way.
+    int exchange_pp(int buf, int rows) {
+        if (!sharded()) return 0;
+        const size_t nx = (size_t)g.nx;
+        float *b = f.pp[buf];
+        const int nyl = g.nyl;
+        RCCL_TRY(ncclGroupStart());
+        if (rank > 0) {
+            RCCL_TRY(ncclSend(b, rows * nx, ncclFloat, rank - 1, comm, stream));
+            RCCL_TRY(ncclRecv(b - (size_t)rows * nx, rows * nx, ncclFloat, rank - 1, comm, stream));
+        }
+        if (rank + 1 < n_ranks) {
+            RCCL_TRY(ncclSend(b + (size_t)(nyl - rows) * nx, rows * nx, ncclFloat, rank + 1, comm,
+                              stream));
+            RCCL_TRY(ncclRecv(b + (size_t)nyl * nx, rows * nx, ncclFloat, rank + 1, comm, stream));
+        }
+        RCCL_TRY(ncclGroupEnd());
+        return 0;
+    }
+
+    int allreduce_max_u32(uint32_t *dev, size_t n) {
+        if (!sharded()) return 0;
+        RCCL_TRY(ncclAllReduce(dev, dev, n, ncclUint32, ncclMax, comm, stream));
+        return 0;
+    }
+
+    // -------------------------------------------------------------- solve
+    // jacobi_pressure (model.rs:734-824).  Unsharded: one launch per sweep
+    // over global rows 1..=ny-2, early exit decided on the device.  Sharded
+    // (tolerance off): halo depth hg, p' exchanged every hg sweeps; between
+    // exchanges each sweep also recomputes a shrinking band of ghost rows, so
+    // results equal the single-domain sweep bit for bit.
+    int enqueue_solve(int pass) {
+        const int iters = params.jacobi_iters;
+        const int lo_g = 1 - (int)j0, hi_g = (int)g.ny - 1 - (int)j0;   // global rows 1..ny-2
+        bool evt = timing && pass <= 0;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (evt) {
+            e0 = take_event();
+            e1 = take_event();
+            HIP_TRY(hipEventRecord(e0, stream));
+        }
+        if (!sharded()) {
+            for (int it = 0; it < iters; ++it)
+                launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
+            if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
+        } else {
+            const int hg = g.hg;
+            for (int it = 0; it < iters; ++it) {
+                const int s = it % hg;
+                const int ext = hg - 1 - s;
+                const int lo = std::max(-ext, lo_g);
+                const int hi = std::min(g.nyl + ext, hi_g);
+                launch_jacobi_sweep(g, f, pass, it, lo, hi, stream);
+                if (s == hg - 1 || it == iters - 1) {
+                    int rc = exchange_pp((host_cur + it + 1) & 1, hg);
+                    if (rc) return rc;
+                }
+            }
+            int rc = allreduce_max_u32(f.ctl->err + (iters > 0 ? iters - 1 : 0), 1);
+            if (rc) return rc;
+        }
+        if (evt && sharded()) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
+        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, stream);
+        HIP_TRY(hipGetLastError());
+        if (evt) {
+            solve_events.emplace_back(e0, e1);
+            timed_sweeps += (uint64_t)iters;
+        }
+        host_cur = (host_cur + iters) & 1;
+        return 0;
+    }
+
+    // Sharded with the tolerance on: the host follows the reference's control
+    // flow, reading the all-reduced residual after every sweep (halo depth 1).
+    int enqueue_solve_host_driven(float *residual_out) {
+        const int iters = params.jacobi_iters;
+        const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
+        int n = 0;
+        for (int it = 0; it < iters; ++it) {
+            launch_jacobi_sweep(g, f, -1, it, lo, hi, stream);
+            int rc = allreduce_max_u32(f.ctl->err + it, 1);
+            if (rc) return rc;
+            rc = exchange_pp((host_cur + it + 1) & 1, 1);
+            if (rc) return rc;
+            ++n;
+            uint32_t bits = 0;
+            HIP_TRY(hipMemcpyAsync(&bits, f.ctl->err + it, 4, hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            float e;
+            std::memcpy(&e, &bits, 4);
+            if (params.tol_enabled && e < params.p_tol) break;
+        }
+        // the device finalize recomputes n from the (identical) all-reduced slots
+        launch_finalize_solve(g, f, -1, iters, 0, stream);
+        HIP_TRY(hipGetLastError());
+        host_cur = (host_cur + n) & 1;
+        float res = 0.f;
+        HIP_TRY(hipMemcpyAsync(&res, &f.ctl->last_p, 4, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (residual_out) *residual_out = res;
+        return 0;
+    }
+
+    bool host_driven() const { return sharded() && params.tol_enabled; }
+
+    // piso_step (model.rs:529-730).
+    int enqueue_piso(float dt_override) {
+        launch_u_predictor(g, f, dt_override, stream);
+        launch_v_predictor(g, f, dt_override, stream);
+        if (!host_driven()) {
+            launch_divergence(g, f, 0, dt_override, stream);
+            int rc = enqueue_solve(0);
+            if (rc) return rc;
+            launch_corrector(g, f, 0, dt_override, stream);
+            for (int pass = 1; pass <= params.corrector_passes; ++pass) {
+                launch_copy_star(g, f, pass, stream);
+                launch_divergence(g, f, pass, dt_override, stream);
+                rc = enqueue_solve(pass);
+                if (rc) return rc;
+                launch_corrector(g, f, pass, dt_override, stream);
+            }
+        } else {
+            launch_divergence(g, f, -1, dt_override, stream);
+            float res = 0.f;
+            int rc = enqueue_solve_host_driven(&res);
+            if (rc) return rc;
+            launch_corrector(g, f, -1, dt_override, stream);
+            for (int pass = 1; pass <= params.corrector_passes; ++pass) {
+                launch_copy_star(g, f, -1, stream);
+                launch_divergence(g, f, -1, dt_override, stream);
+                rc = enqueue_solve_host_driven(&res);
+                if (rc) return rc;
+                launch_corrector(g, f, -1, dt_override, stream);
+                if (res < params.p_tol) break;
+            }
+        }
+        launch_boundary(g, f, stream);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+
+    // Model::update (model.rs:304-379).
+    int enqueue_update() {
+        if (timing) {
+            hipEvent_t e0 = take_event();
+            HIP_TRY(hipEventRecord(e0, stream));
+            step_events.push_back(e0);
+        }
+        HIP_TRY(hipEventRecord(ev_step0, stream));
+        launch_step_begin(g, f, stream);
+        int rc = exchange_uv();
+        if (rc) return rc;
+        rc = enqueue_piso(kNaN);
+        if (rc) return rc;
+        launch_step_reduce(g, f, stream);
+        rc = allreduce_max_u32(f.ctl->red, 4);
+        if (rc) return rc;
+        launch_step_finalize(g, f, stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ev_step1, stream));
+        if (timing) {
+            hipEvent_t e1 = take_event();
+            HIP_TRY(hipEventRecord(e1, stream));
+            step_events.push_back(e1);
+            timed_steps++;
+        }
+        stepped = true;
+        return 0;
+    }
+    std::vector<hipEvent_t> step_events;
+
+    int sync() {
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipStreamSynchronize(stream));
+        return 0;
+    }
+
+    int read_ctl(Ctl *out) {
+        int rc = sync();
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy(out, f.ctl, offsetof(Ctl, go), hipMemcpyDeviceToHost));
+        return 0;
+    }
+
+    void destroy() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (comm) ncclCommDestroy(comm);
+        for (void *ptr : {(void *)u_all, (void *)v_all, (void *)uo_all, (void *)vo_all,
+                          (void *)us_all, (void *)vs_all, (void *)p, (void *)rhs,
+                          (void *)pp_all[0], (void *)pp_all[1], (void *)mask_u, (void *)mask_v,
+                          (void *)obs, (void *)ctl})
+            if (ptr) (void)hipFree(ptr);
+        for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+        if (ev_step0) (void)hipEventDestroy(ev_step0);
+        if (ev_step1) (void)hipEventDestroy(ev_step1);
+        if (ev_prof0) (void)hipEventDestroy(ev_prof0);
+        if (ev_prof1) (void)hipEventDestroy(ev_prof1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+int validate(const cfd_grid *grid, const cfd_params *p) {
+    if (!grid || !p) return fail(CFD_EINVAL, "null grid or params");
+    if (grid->nx < 16 || grid->nx % 8 != 0)
+        return fail(CFD_EINVAL, "nx must be a multiple of 8 and >= 16 (model.rs:541 precondition)");
+    if (grid->ny < 4) return fail(CFD_EINVAL, "ny must be >= 4");
+    if ((grid->nx + 1) * grid->ny > (1ull << 31))
+        return fail(CFD_EINVAL, "grid too large for 32-bit row indexing");
+    if (!(grid->lx > 0.f) || !(grid->ly > 0.f)) return fail(CFD_EINVAL, "lx, ly must be > 0");
+    if (p->jacobi_iters < 0 || p->jacobi_iters > kMaxSweeps)
+        return fail(CFD_EINVAL, "jacobi_iters out of range [0, 4096]");
+    if (p->corrector_passes < 0 || p->corrector_passes > kMaxPasses - 1)
+        return fail(CFD_EINVAL, "corrector_passes out of range [0, 63]");
+    if (p->velocity_scheme != 0 && p->velocity_scheme != 1)
+        return fail(CFD_EINVAL, "velocity_scheme must be 0 or 1");
+    if (p->inlet_profile != 0 && p->inlet_profile != 1)
+        return fail(CFD_EINVAL, "inlet_profile must be 0 or 1");
+    if (p->pressure_solver != 0) return fail(CFD_EINVAL, "pressure_solver must be 0 (Jacobi)");
+    if (p->bc_kind != 0 && p->bc_kind != 1) return fail(CFD_EINVAL, "bc_kind must be 0 or 1");
+    return 0;
+}
+
+void apply_params(cfd_model *m, const cfd_params *p) {
+    m->params = *p;
+    m->g.nu = p->viscosity;
+    m->g.target_inlet = p->target_inlet_velocity;
+    m->g.scheme = p->velocity_scheme;
+    m->g.profile = p->inlet_profile;
+    m->g.bc_kind = p->bc_kind;
+    m->g.tol_enabled = p->tol_enabled ? 1 : 0;
+    m->g.p_tol = p->p_tol;
+    m->g.jacobi_iters = p->jacobi_iters;
+}
+
+// Model::new (model.rs:219-299), restricted to rows [j0, j1) of the slab.
+int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int device, int hg) {
+    m->device = device;
+    m->grid = *grid;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&m->ev_step0));
+    HIP_TRY(hipEventCreate(&m->ev_step1));
+    HIP_TRY(hipEventCreate(&m->ev_prof0));
+    HIP_TRY(hipEventCreate(&m->ev_prof1));
+    const int nx = (int)grid->nx, ny = (int)grid->ny;
+    Geom &g = m->g;
+    g.nx = nx;
+    g.ny = ny;
+    g.j0 = (int)m->j0;
+    g.nyl = (int)(m->j1 - m->j0);
+    g.hg = hg;
+    g.dx = grid->lx / (float)grid->nx;   // src/app.rs:37
+    g.dy = grid->ly / (float)grid->ny;   // src/app.rs:38
+    g.ly = grid->ly;
+    apply_params(m, p);
+
+    const size_t W = (size_t)nx + 1, nyl = (size_t)g.nyl;
+    const size_t u_alloc = round4(m->u_rows_alloc() * W);
+    const size_t v_alloc = round4(m->v_rows_alloc() * (size_t)nx);
+    const size_t p_n = nyl * nx;
+    const size_t pp_n = (nyl + 2 * (size_t)hg) * nx;
+    auto zalloc = [&](void **ptr, size_t bytes) -> int {
+        HIP_TRY(hipMalloc(ptr, bytes));
+        HIP_TRY(hipMemsetAsync(*ptr, 0, bytes, m->stream));
+        return 0;
+    };
+    int rc = 0;
+    if ((rc = zalloc((void **)&m->u_all, u_alloc * 4)) || (rc = zalloc((void **)&m->v_all, v_alloc * 4)) ||
+        (rc = zalloc((void **)&m->uo_all, u_alloc * 4)) || (rc = zalloc((void **)&m->vo_all, v_alloc * 4)) ||
+        (rc = zalloc((void **)&m->us_all, u_alloc * 4)) || (rc = zalloc((void **)&m->vs_all, v_alloc * 4)) ||
+        (rc = zalloc((void **)&m->p, p_n * 4)) || (rc = zalloc((void **)&m->rhs, p_n * 4)) ||
+        (rc = zalloc((void **)&m->pp_all[0], pp_n * 4)) || (rc = zalloc((void **)&m->pp_all[1], pp_n * 4)) ||
+        (rc = zalloc((void **)&m->mask_u, nyl * W + 16)) || (rc = zalloc((void **)&m->mask_v, (nyl + 1) * nx + 16)) ||
+        (rc = zalloc((void **)&m->ctl, sizeof(Ctl))))
+        return rc;
+
+    // obstacle masks and cell list from cell centres (model.rs:235-260)
+    std::vector<uint8_t> mu(nyl * W, 0), mv((nyl + 1) * nx, 0);
+    std::vector<int32_t> obs;
+    if (grid->has_cylinder) {
+        for (int j = 0; j < ny; ++j) {
+            for (int i = 0; i < nx; ++i) {
+                const float x = ((float)i + 0.5f) * g.dx;
+                const float y = ((float)j + 0.5f) * g.dy;
+                const float ddx = x - grid->cylinder_x;
+                const float ddy = y - grid->cylinder_y;
+                const float distance = std::sqrt(ddx * ddx + ddy * ddy);
+                if (!(distance < grid->cylinder_radius)) continue;
+                const long lj = (long)j - (long)m->j0;
+                if (lj >= 0 && lj < (long)nyl) {
+                    if (i > 0) mu[lj * W + i] = 1;
+                    if (i < nx) mu[lj * W + i + 1] = 1;
+                }
+                if (j > 0 && lj >= 0 && lj <= (long)nyl) mv[lj * nx + i] = 1;
+                if (j < ny && lj + 1 >= 0 && lj + 1 <= (long)nyl) mv[(lj + 1) * nx + i] = 1;
+                if (lj >= 0 && lj <= (long)nyl) {
+                    obs.push_back(i);
+                    obs.push_back(j);
+                }
+            }
+        }
+    }
+    m->h_mask_u = mu;
+    m->h_mask_v = mv;
+    HIP_TRY(hipMemcpyAsync(m->mask_u, mu.data(), mu.size(), hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipMemcpyAsync(m->mask_v, mv.data(), mv.size(), hipMemcpyHostToDevice, m->stream));
+    if (!obs.empty()) {
+        HIP_TRY(hipMalloc((void **)&m->obs, obs.size() * 4));
+        HIP_TRY(hipMemcpyAsync(m->obs, obs.data(), obs.size() * 4, hipMemcpyHostToDevice, m->stream));
+    }
+
+    Fields &f = m->f;
+    const size_t uoff = (size_t)kGhostUV * W, voff = (size_t)kGhostUV * nx;
+    f.u_alloc_base = m->u_all;
+    f.v_alloc_base = m->v_all;
+    f.u_old_base = m->uo_all;
+    f.v_old_base = m->vo_all;
+    f.u_star_base = m->us_all;
+    f.v_star_base = m->vs_all;
+    f.u_alloc = u_alloc;
+    f.v_alloc = v_alloc;
+    f.u = m->u_all + uoff;
+    f.v = m->v_all + voff;
+    f.u_old = m->uo_all + uoff;
+    f.v_old = m->vo_all + voff;
+    f.u_star = m->us_all + uoff;
+    f.v_star = m->vs_all + voff;
+    f.p = m->p;
+    f.rhs = m->rhs;
+    f.pp[0] = m->pp_all[0] + (size_t)hg * nx;
+    f.pp[1] = m->pp_all[1] + (size_t)hg * nx;
+    f.mask_u = m->mask_u;
+    f.mask_v = m->mask_v;
+    f.obs = m->obs;
+    f.n_obs = (int32_t)(obs.size() / 2);
+    f.ctl = m->ctl;
+
+    Ctl c0;
+    std::memset(&c0, 0, sizeof(c0));
+    c0.dt = p->dt;
+    c0.go[0] = 1;
+    HIP_TRY(hipMemcpyAsync(m->ctl, &c0, sizeof(Ctl), hipMemcpyHostToDevice, m->stream));
+    HIP_TRY(hipStreamSynchronize(m->stream));
+    return 0;
+}
+
+int create_common(const cfd_grid *grid, const cfd_params *params, int device, int n_ranks, int rank,
+                  const void *uid, cfd_model **out) {
+    if (!out) return fail(CFD_EINVAL, "null out");
+    *out = nullptr;
+    int rc = validate(grid, params);
+    if (rc) return rc;
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad rank/n_ranks");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CFD_EHIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(CFD_EINVAL, "device ordinal out of range");
+    cfd_model *m = new cfd_model();
+    m->n_ranks = n_ranks;
+    m->rank = rank;
+    slab_rows(grid->ny, n_ranks, rank, &m->j0, &m->j1);
+    int hg = 1;
+    if (n_ranks > 1) {
+        const char *env = getenv("CFD_HALO_DEPTH");
+        hg = env ? atoi(env) : 8;
+        if (hg < 1) hg = 1;
+        uint64_t min_rows = grid->ny / (uint64_t)n_ranks;
+        if ((uint64_t)hg + 2 > min_rows) hg = (int)(min_rows > 3 ? min_rows - 2 : 1);
+        if (min_rows < 4) {
+            delete m;
+            return fail(CFD_EINVAL, "each slab needs at least 4 rows");
+        }
+    }
+    rc = build_model(m, grid, params, device, hg);
+    if (!rc && n_ranks > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, uid, sizeof(id));
+        ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, id, rank);
+        if (r != ncclSuccess) rc = fail(CFD_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    if (rc) {
+        m->destroy();
+        delete m;
+        return rc;
+    }
+    *out = m;
+    return 0;
+}
+
+}  // namespace
+
+// =============================================================== C ABI
+
+extern "C" {
+
+const char *cfd_last_error(void) { return g_last_error.c_str(); }
+int cfd_abi_version(void) { return CFD_ABI_VERSION; }
+
+void cfd_default_params(cfd_params *o) {
+    if (!o) return;
+    o->dt = 0.005f;                  // model.rs:47
+    o->viscosity = 0.000001f;        // model.rs:48
+    o->target_inlet_velocity = 1.0f; // model.rs:49
+    o->velocity_scheme = CFD_SCHEME_FIRST_ORDER;
+    o->inlet_profile = CFD_INLET_UNIFORM;
+    o->pressure_solver = CFD_SOLVER_JACOBI;
+    o->jacobi_iters = 50;            // model.rs:737
+    o->corrector_passes = 20;        // model.rs:696
+    o->tol_enabled = 1;
+    o->p_tol = 1e-4f;                // model.rs:736, 721
+    o->bc_kind = CFD_BC_CHANNEL;
+}
+
+void cfd_default_grid(cfd_grid *o) {
+    if (!o) return;
+    o->nx = 800;                     // src/app.rs:34
+    o->ny = 264;
+    o->lx = 30.0f;
+    o->ly = 10.0f;
+    o->has_cylinder = 1;
+    o->cylinder_x = 30.0f / 4.0f;    // src/app.rs:47
+    o->cylinder_y = 10.0f / 2.0f;
+    o->cylinder_radius = 0.75f;
+}
+
+int cfd_create(const cfd_grid *grid, const cfd_params *params, int device_ordinal, cfd_model **out) {
+    return create_common(grid, params, device_ordinal, 1, 0, nullptr, out);
+}
+
+int cfd_rccl_unique_id(void *out) {
+    if (!out) return fail(CFD_EINVAL, "null out");
+    ncclUniqueId id;
+    RCCL_TRY(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out, &id, sizeof(id));
+    return 0;
+}
+
+int cfd_create_sharded(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
+                       int n_ranks, int rank, const void *uid, cfd_model **out) {
+    if (n_ranks > 1 && !uid) return fail(CFD_EINVAL, "null rccl unique id");
+    return create_common(grid, params, device_ordinal, n_ranks, rank, uid, out);
+}
+
+int cfd_get_slab(const cfd_model *m, uint64_t *j0, uint64_t *j1) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (j0) *j0 = m->j0;
+    if (j1) *j1 = m->j1;
+    return 0;
+}
+
+int cfd_update(cfd_model *m) { return cfd_update_n(m, 1); }
+
+int cfd_update_n(cfd_model *m, int n) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    HIP_TRY(hipSetDevice(m->device));
+    for (int k = 0; k < n; ++k) {
+        int rc = m->enqueue_update();
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int cfd_piso_step(cfd_model *m, float dt_sub) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    HIP_TRY(hipSetDevice(m->device));
+    int rc = m->exchange_uv();
+    if (rc) return rc;
+    return m->enqueue_piso(dt_sub);
+}
+
+int cfd_pressure_solve(cfd_model *m, float *residual_out) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    HIP_TRY(hipSetDevice(m->device));
+    int rc;
+    if (m->host_driven()) {
+        return m->enqueue_solve_host_driven(residual_out);
+    }
+    rc = m->enqueue_solve(-1);
+    if (rc) return rc;
+    Ctl c;
+    rc = m->read_ctl(&c);
+    if (rc) return rc;
+    if (residual_out) *residual_out = c.last_p;
+    return 0;
+}
+
+int cfd_run_phase(cfd_model *m, int phase, float dt_sub) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    HIP_TRY(hipSetDevice(m->device));
+    switch (phase) {
+    case CFD_PHASE_U_PREDICTOR: {
+        int rc = m->exchange_uv();
+        if (rc) return rc;
+        launch_u_predictor(m->g, m->f, dt_sub, m->stream);
+        break;
+    }
+    case CFD_PHASE_V_PREDICTOR: {
+        int rc = m->exchange_uv();
+        if (rc) return rc;
+        launch_v_predictor(m->g, m->f, dt_sub, m->stream);
+        break;
+    }
+    case CFD_PHASE_DIVERGENCE: launch_divergence(m->g, m->f, -1, dt_sub, m->stream); break;
+    case CFD_PHASE_CORRECTOR: launch_corrector(m->g, m->f, -1, dt_sub, m->stream); break;
+    case CFD_PHASE_BOUNDARY: launch_boundary(m->g, m->f, m->stream); break;
+    default: return fail(CFD_EINVAL, "unknown phase");
+    }
+    HIP_TRY(hipGetLastError());
+    return m->sync();
+}
+
+int cfd_set_params(cfd_model *m, const cfd_params *p) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    int rc = validate(&m->grid, p);
+    if (rc) return rc;
+    rc = m->sync();
+    if (rc) return rc;
+    if (!p->tol_enabled && m->params.tol_enabled) {
+        // host mirror of the current p' buffer is needed again
+        Ctl c;
+        rc = m->read_ctl(&c);
+        if (rc) return rc;
+        m->host_cur = c.cur;
+    }
+    apply_params(m, p);
+    // set_parameters overwrites dt (model.rs:1252)
+    HIP_TRY(hipMemcpy(&m->ctl->dt, &p->dt, 4, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int cfd_get_snapshot(cfd_model *m, float *u, float *v, float *p, float *dt_out) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    int rc = m->sync();
+    if (rc) return rc;
+    const size_t W = (size_t)m->g.nx + 1, nx = (size_t)m->g.nx, nyl = (size_t)m->g.nyl;
+    if (u) HIP_TRY(hipMemcpy(u, m->f.u, nyl * W * 4, hipMemcpyDeviceToHost));
+    if (v) HIP_TRY(hipMemcpy(v, m->f.v, (nyl + 1) * nx * 4, hipMemcpyDeviceToHost));
+    if (p) HIP_TRY(hipMemcpy(p, m->f.p, nyl * nx * 4, hipMemcpyDeviceToHost));
+    if (dt_out) HIP_TRY(hipMemcpy(dt_out, &m->ctl->dt, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int cfd_get_residuals(cfd_model *m, cfd_residuals *out) {
+    if (!m || !out) return fail(CFD_EINVAL, "null argument");
+    Ctl c;
+    int rc = m->read_ctl(&c);
+    if (rc) return rc;
+    out->simulation_step = c.step;
+    out->simulation_time = c.time;
+    out->dt = c.dt;
+    out->p = c.last_p;
+    out->u = c.res_u;
+    out->v = c.res_v;
+    out->piso_substeps = 1;   // substep_count (model.rs:267)
+    out->jacobi_sweeps_total = c.sweeps_total;
+    float ms = 0.f;
+    if (m->stepped && hipEventElapsedTime(&ms, m->ev_step0, m->ev_step1) == hipSuccess)
+        out->step_time_s = ms * 1e-3;
+    else
+        out->step_time_s = 0.0;
+    return 0;
+}
+
+int cfd_get_state(cfd_model *m, cfd_state *st) {
+    if (!m || !st) return fail(CFD_EINVAL, "null argument");
+    Ctl c;
+    int rc = m->read_ctl(&c);
+    if (rc) return rc;
+    const size_t W = (size_t)m->g.nx + 1, nx = (size_t)m->g.nx, nyl = (size_t)m->g.nyl;
+    if (st->u) HIP_TRY(hipMemcpy(st->u, m->f.u, nyl * W * 4, hipMemcpyDeviceToHost));
+    if (st->v) HIP_TRY(hipMemcpy(st->v, m->f.v, (nyl + 1) * nx * 4, hipMemcpyDeviceToHost));
+    if (st->p) HIP_TRY(hipMemcpy(st->p, m->f.p, nyl * nx * 4, hipMemcpyDeviceToHost));
+    if (st->u_star) HIP_TRY(hipMemcpy(st->u_star, m->f.u_star, nyl * W * 4, hipMemcpyDeviceToHost));
+    if (st->v_star) HIP_TRY(hipMemcpy(st->v_star, m->f.v_star, (nyl + 1) * nx * 4, hipMemcpyDeviceToHost));
+    if (st->p_prime) HIP_TRY(hipMemcpy(st->p_prime, m->f.pp[c.cur], nyl * nx * 4, hipMemcpyDeviceToHost));
+    if (st->rhs) HIP_TRY(hipMemcpy(st->rhs, m->f.rhs, nyl * nx * 4, hipMemcpyDeviceToHost));
+    st->dt = c.dt;
+    st->simulation_time = c.time;
+    st->simulation_step = c.step;
+    st->last_p_residual = c.last_p;
+    st->last_u_residual = c.res_u;
+    st->last_v_residual = c.res_v;
+    st->jacobi_sweeps_total = c.sweeps_total;
+    return 0;
+}
+
+int cfd_set_state(cfd_model *m, const cfd_state *st) {
+    if (!m || !st) return fail(CFD_EINVAL, "null argument");
+    Ctl c;
+    int rc = m->read_ctl(&c);
+    if (rc) return rc;
+    const size_t W = (size_t)m->g.nx + 1, nx = (size_t)m->g.nx, nyl = (size_t)m->g.nyl;
+    if (st->u) HIP_TRY(hipMemcpy(m->f.u, st->u, nyl * W * 4, hipMemcpyHostToDevice));
+    if (st->v) HIP_TRY(hipMemcpy(m->f.v, st->v, (nyl + 1) * nx * 4, hipMemcpyHostToDevice));
+    if (st->p) HIP_TRY(hipMemcpy(m->f.p, st->p, nyl * nx * 4, hipMemcpyHostToDevice));
+    if (st->u_star) HIP_TRY(hipMemcpy(m->f.u_star, st->u_star, nyl * W * 4, hipMemcpyHostToDevice));
+    if (st->v_star) HIP_TRY(hipMemcpy(m->f.v_star, st->v_star, (nyl + 1) * nx * 4, hipMemcpyHostToDevice));
+    if (st->p_prime) HIP_TRY(hipMemcpy(m->f.pp[c.cur], st->p_prime, nyl * nx * 4, hipMemcpyHostToDevice));
+    if (st->rhs) HIP_TRY(hipMemcpy(m->f.rhs, st->rhs, nyl * nx * 4, hipMemcpyHostToDevice));
+    c.dt = st->dt;
+    c.time = st->simulation_time;
+    c.step = (uint32_t)st->simulation_step;
+    c.last_p = st->last_p_residual;
+    c.res_u = st->last_u_residual;
+    c.res_v = st->last_v_residual;
+    c.sweeps_total = st->jacobi_sweeps_total;
+    HIP_TRY(hipMemcpy(m->f.ctl, &c, offsetof(Ctl, go), hipMemcpyHostToDevice));
+    m->host_cur = c.cur;
+    // ghosts of the injected slab
+    rc = m->exchange_uv();
+    if (rc) return rc;
+    rc = m->exchange_pp(c.cur, m->g.hg);
+    if (rc) return rc;
+    return m->sync();
+}
+
+int cfd_get_masks(cfd_model *m, uint8_t *mask_u, uint8_t *mask_v) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (mask_u) std::memcpy(mask_u, m->h_mask_u.data(), m->h_mask_u.size());
+    if (mask_v) std::memcpy(mask_v, m->h_mask_v.data(), m->h_mask_v.size());
+    return 0;
+}
+
+int cfd_synchronize(cfd_model *m) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    return m->sync();
+}
+
+int cfd_profile_sweeps(cfd_model *m, int n_sweeps, double *avg_ms_out) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (n_sweeps < 1 || n_sweeps > kMaxSweeps) return fail(CFD_EINVAL, "n_sweeps out of range");
+    HIP_TRY(hipSetDevice(m->device));
+    const int lo = std::max(0, 1 - (int)m->j0), hi = std::min(m->g.nyl, (int)m->g.ny - 1 - (int)m->j0);
+    hipEvent_t a = m->ev_prof0, b = m->ev_prof1;
+    Geom g = m->g;
+    g.tol_enabled = 0;
+    HIP_TRY(hipEventRecord(a, m->stream));
+    for (int it = 0; it < n_sweeps; ++it) launch_jacobi_sweep(g, m->f, -1, it, lo, hi, m->stream);
+    HIP_TRY(hipEventRecord(b, m->stream));
+    launch_finalize_solve(g, m->f, -1, n_sweeps, 0, m->stream);
+    HIP_TRY(hipGetLastError());
+    m->host_cur = (m->host_cur + n_sweeps) & 1;
+    int rc = m->sync();
+    if (rc) return rc;
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    if (avg_ms_out) *avg_ms_out = ms / n_sweeps;
+    return 0;
+}
+
+// Timing of the pressure solves inside cfd_update (HIP events on the model's
+// stream): enable, run steps, then read the totals.
+int cfd_timing_begin(cfd_model *m) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    int rc = m->sync();
+    if (rc) return rc;
+    m->timing = true;
+    m->ev_next = 0;
+    m->solve_events.clear();
+    m->step_events.clear();
+    m->timed_sweeps = 0;
+    m->timed_steps = 0;
+    return 0;
+}
+
+int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *step_ms, uint64_t *steps) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    int rc = m->sync();
+    if (rc) return rc;
+    double s_ms = 0.0, t_ms = 0.0;
+    for (auto &pr : m->solve_events) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+        s_ms += ms;
+    }
+    for (size_t k = 0; k + 1 < m->step_events.size(); k += 2) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, m->step_events[k], m->step_events[k + 1]));
+        t_ms += ms;
+    }
+    if (solve_ms) *solve_ms = s_ms;
+    if (sweeps) *sweeps = m->timed_sweeps;
+    if (step_ms) *step_ms = t_ms;
+    if (steps) *steps = m->timed_steps;
+    m->timing = false;
+    m->ev_next = 0;
+    m->solve_events.clear();
+    m->step_events.clear();
+    return 0;
+}
+
+int cfd_get_halo_depth(const cfd_model *m) { return m ? m->g.hg : 0; }
+
+void cfd_destroy(cfd_model *m) {
+    if (!m) return;
+    m->destroy();
+    delete m;
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+/*
+ * cfd.h — C ABI of the MI355X-native pressure-projection hot path of
+ * TSultanov/cfd-demo (src/model.rs).  Plain C types only: an opaque handle,
+ * POD structs, float/uint8 pointers and sizes.  No torch or HIP types cross
+ * this boundary.
+ *
+ * Each entry point replaces one method of the reference's `Model`
+ * (/root/reference/src/model.rs); the citation is given per function.  The
+ * reference has no FFI of its own; INTEGRATION.md shows the Rust `extern "C"`
+ * block and wrapper a maintainer would add to keep src/app.rs unchanged.
+ *
+ * Conventions
+ *   - return 0 on success, a negative cfd_status on failure; cfd_last_error()
+ *     returns a thread-local message for the last failure on this thread.
+ *   - a handle is thread-affine (the reference moves Model into one worker
+ *     thread, model.rs:1287); calls on one handle must not race.
+ *   - host buffers are caller-owned; sizes follow the reference's flat
+ *     row-major layout (model.rs:161-214):
+ *        u: (nx+1)*ny   v: nx*(ny+1)   p, rhs, p_prime: nx*ny
+ *     For a sharded model (cfd_create_sharded) every host buffer covers the
+ *     rank's slab only: pressure rows [j0, j1) (cfd_get_slab), u rows
+ *     [j0, j1), v rows [j0, j1] (the shared face row j1 is held by both
+ *     neighbouring ranks).
+ *   - the precondition nx % 8 == 0 of the reference's 8-lane loops
+ *     (model.rs:541, 402-403) is enforced: other shapes return CFD_EINVAL.
+ *   - cfd_update / cfd_update_n are asynchronous: they enqueue the step on the
+ *     model's HIP stream and return.  Reading calls (snapshot, state,
+ *     residuals) synchronise.
+ */
+#ifndef CFD_H
+#define CFD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFD_ABI_VERSION 1
+
+typedef enum {
+    CFD_OK = 0,
+    CFD_EINVAL = -1,   /* bad argument or unsupported shape (nx % 8 != 0, ...) */
+    CFD_EHIP = -2,     /* HIP runtime error (no device, out of memory, launch) */
+    CFD_ERCCL = -3,    /* RCCL error (sharded models only) */
+    CFD_ESTATE = -4,   /* call not valid in the model's current state */
+} cfd_status;
+
+typedef struct cfd_model cfd_model;
+
+/* Grid + optional Cylinder (model.rs:119-139).  dx = lx/nx and dy = ly/ny
+ * are derived exactly as src/app.rs:37-38 does. */
+typedef struct {
+    uint64_t nx, ny;
+    float lx, ly;
+    int32_t has_cylinder;
+    float cylinder_x, cylinder_y, cylinder_radius;
+} cfd_grid;
+
+/* SimulationParams (model.rs:13-21) + this build's knobs.  Reference
+ * behaviour is jacobi_iters 50, corrector_passes 20, tol_enabled 1,
+ * p_tol 1e-4, bc_kind CFD_BC_CHANNEL. */
+enum { CFD_SCHEME_FIRST_ORDER = 0, CFD_SCHEME_SECOND_ORDER = 1 };
+enum { CFD_INLET_UNIFORM = 0, CFD_INLET_PARABOLIC = 1 };
+enum { CFD_SOLVER_JACOBI = 0 };
+enum { CFD_BC_CHANNEL = 0, CFD_BC_CAVITY = 1 };
+typedef struct {
+    float dt;
+    float viscosity;
+    float target_inlet_velocity;   /* channel: inlet U; cavity: lid U */
+    int32_t velocity_scheme;
+    int32_t inlet_profile;
+    int32_t pressure_solver;
+    int32_t jacobi_iters;          /* sweeps per pressure solve (model.rs:737) */
+    int32_t corrector_passes;      /* extra correction passes (model.rs:696) */
+    int32_t tol_enabled;           /* early exits at p_tol (model.rs:816, 721) */
+    float p_tol;
+    int32_t bc_kind;
+} cfd_params;
+
+/* Residuals (model.rs:23-32). step_time_s is device time of the last step
+ * measured with HIP events. */
+typedef struct {
+    uint64_t simulation_step;
+    float simulation_time;
+    float dt;
+    float p, u, v;
+    double step_time_s;
+    uint32_t piso_substeps;
+    uint64_t jacobi_sweeps_total;
+} cfd_residuals;
+
+/* Full persistent state: enough to resume bit-exactly.
+ * Any pointer may be NULL to skip that field. */
+typedef struct {
+    float *u, *v, *p, *u_star, *v_star, *p_prime, *rhs;
+    float dt;
+    float simulation_time;
+    uint64_t simulation_step;
+    float last_p_residual, last_u_residual, last_v_residual;
+    uint64_t jacobi_sweeps_total;
+} cfd_state;
+
+/* SimulationParams::default() (model.rs:44-55) + reference knob values. */
+void cfd_default_params(cfd_params *out);
+/* default_grid() (src/app.rs:32-53): 800 x 264, 30 x 10, cylinder r 0.75. */
+void cfd_default_grid(cfd_grid *out);
+
+/* Model::new (model.rs:219-299) on HIP device `device_ordinal`. */
+int cfd_create(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
+               cfd_model **out);
+
+/* 1D row-slab decomposition over n_ranks processes (one per GPU).  Rank 0
+ * calls cfd_rccl_unique_id and distributes the 128 bytes out of band
+ * (bench.py uses torch.distributed).  Results are bitwise identical to the
+ * single-GPU model: the path has no sums across ranks, only halo copies and
+ * exact maxima. */
+int cfd_rccl_unique_id(void *out_128_bytes);
+int cfd_create_sharded(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
+                       int n_ranks, int rank, const void *rccl_unique_id, cfd_model **out);
+/* Global pressure rows [j0, j1) held by this model (0, ny for cfd_create). */
+int cfd_get_slab(const cfd_model *m, uint64_t *j0, uint64_t *j1);
+
+/* Model::update (model.rs:304-379): one time step, asynchronous. */
+int cfd_update(cfd_model *m);
+/* n consecutive Model::update calls, enqueued without host round trips. */
+int cfd_update_n(cfd_model *m, int n);
+/* piso_step (model.rs:529-730) with an explicit dt_sub; no u_old copy, no
+ * residual/CFL bookkeeping. */
+int cfd_piso_step(cfd_model *m, float dt_sub);
+/* jacobi_pressure (model.rs:734-824) on the current rhs and p_prime.
+ * Synchronous; writes the returned max |dp'| to *residual_out (may be NULL). */
+int cfd_pressure_solve(cfd_model *m, float *residual_out);
+
+/* Single phases of piso_step, for known-answer tests. */
+enum {
+    CFD_PHASE_U_PREDICTOR = 0,   /* model.rs:538-580   */
+    CFD_PHASE_V_PREDICTOR = 1,   /* model.rs:586-670   */
+    CFD_PHASE_DIVERGENCE = 2,    /* model.rs:1406-1440 */
+    CFD_PHASE_CORRECTOR = 3,     /* model.rs:1334-1404 */
+    CFD_PHASE_BOUNDARY = 4,      /* model.rs:826-875   */
+};
+int cfd_run_phase(cfd_model *m, int phase, float dt_sub);
+
+/* set_parameters (model.rs:1250-1257). */
+int cfd_set_params(cfd_model *m, const cfd_params *params);
+/* get_snapshot (model.rs:1259-1267): copies u, v, p (NULL skips) and dt. */
+int cfd_get_snapshot(cfd_model *m, float *u, float *v, float *p, float *dt_out);
+/* get_residuals (model.rs:1269-1280). */
+int cfd_get_residuals(cfd_model *m, cfd_residuals *out);
+/* Whole state, for fixtures and checkpoint/resume. */
+int cfd_get_state(cfd_model *m, cfd_state *st);
+int cfd_set_state(cfd_model *m, const cfd_state *st);
+/* Obstacle masks as built by Model::new (u8, u and v layouts). */
+int cfd_get_masks(cfd_model *m, uint8_t *mask_u, uint8_t *mask_v);
+
+/* Wait for all work enqueued on the model's stream. */
+int cfd_synchronize(cfd_model *m);
+/* Last Jacobi kernel duration in ms averaged over the sweeps of the most
+ * recent cfd_profile_sweeps() call; measured with HIP events on the
+ * model's stream. */
+int cfd_profile_sweeps(cfd_model *m, int n_sweeps, double *avg_ms_out);
+
+/* Event timing of the pressure solves and whole steps inside cfd_update:
+ * cfd_timing_begin starts recording, cfd_timing_end synchronises and returns
+ * the summed solve time, sweeps timed, summed step time and steps timed. */
+int cfd_timing_begin(cfd_model *m);
+int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *step_ms,
+                   uint64_t *steps);
+/* p' halo depth (rows exchanged per RCCL round) of a sharded model. */
+int cfd_get_halo_depth(const cfd_model *m);
+
+const char *cfd_last_error(void);
+int cfd_abi_version(void);
+void cfd_destroy(cfd_model *m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFD_H */

@@ -459,7 +459,25 @@ void orc_divergence(orc_model *m, float dt_sub) {
 
 /* jacobi_pressure (model.rs:734-824).  The residual is taken only over the
  * SIMD chunks (columns 1..=nx-8 when nx % 8 == 0): the scalar tail chunk
- * (:755-772) never updates max_error.  p' is warm-started (never zeroed). */
+ * (:755-772) never updates max_error.  Per chunk the reference keeps
+ * max_error = max(max_error, reduce_max(|new - center|)) with reduce_max
+ * ignoring NaN lanes and `error > max_error` false for NaN; that is exactly a
+ * running `if (e > max_error) max_error = e` over the chunk columns, which is
+ * how it is written here (and lets the compiler vectorise the row loop like
+ * the reference's 8-lane SIMD).  p' is warm-started (never zeroed). */
+static inline float jac_point(const float *pp, const float *rhs, size_t idx, size_t nx,
+                              float dx_sq, float dy_sq, float denom, float omega, float om1) {
+    float right = pp[idx + 1];
+    float left = pp[idx - 1];
+    float top = pp[idx + nx];
+    float bot = pp[idx - nx];
+    float center = pp[idx];
+    float horizontal = (right + left) / dx_sq;
+    float vertical = (top + bot) / dy_sq;
+    float p_update = (horizontal + vertical - rhs[idx]) / denom;
+    return omega * p_update + om1 * center;
+}
+
 float orc_jacobi_pressure(orc_model *m) {
     size_t nx = m->nx, ny = m->ny;
     float dx = m->dx, dy = m->dy;
@@ -470,60 +488,46 @@ float orc_jacobi_pressure(orc_model *m) {
     const float om1 = 1.0f - jacobi_omega;
     const float denom = 2.0f / (dx * dx) + 2.0f / (dy * dy);
     const float *rhs = m->f[ORC_RHS];
+    /* columns covered by full 8-lane chunks: i in [1, simd_end) */
+    size_t simd_end = 1;
+    while (simd_end + LANES <= nx - 1) simd_end += LANES;
+    /* per-column running maxima (element-wise, so the row loop vectorises) */
+    float *colmax = (float *)malloc((nx + 8) * sizeof(float));
     for (int iter = 0; iter < m->jacobi_iters; ++iter) {
-        float *pp = m->f[ORC_PP], *ppn = m->f[ORC_PPN];
-        max_error = 0.0f;
+        const float *pp = m->f[ORC_PP];
+        float *ppn = m->f[ORC_PPN];
+        for (size_t i = 0; i < nx; ++i) colmax[i] = 0.0f;
         for (size_t j = 1; j < ny - 1; ++j) {
-            for (size_t i = 1; i < nx - 1; i += LANES) {
-                size_t stride = j * nx + i;
-                int tail = (i + LANES > nx - 1);
-                size_t nl = tail ? (nx - i) : LANES;
-                float chunk_max = 0.0f;
-                int chunk_has = 0;
-                for (size_t k = 0; k < nl; ++k) {
-                    size_t idx = stride + k;
-                    float right = pp[idx + 1];
-                    float left = pp[idx - 1];
-                    float top = pp[idx + nx];
-                    float bot = pp[idx - nx];
-                    float center = pp[idx];
-                    float r = rhs[idx];
-                    float horizontal = (right + left) / dx_sq;
-                    float vertical = (top + bot) / dy_sq;
-                    float p_update = (horizontal + vertical - r) / denom;
-                    float new_val = jacobi_omega * p_update + om1 * center;
-                    ppn[idx] = new_val;
-                    if (!tail) {
-                        /* (new - center).abs().reduce_max(): NaN lanes are
-                         * ignored unless all lanes are NaN. */
-                        float e = fabsf(new_val - center);
-                        if (!chunk_has) {
-                            chunk_max = e;
-                            chunk_has = 1;
-                        } else {
-                            chunk_max = fmaxf(chunk_max, e);
-                        }
-                    }
-                }
-                if (!tail && chunk_max > max_error) max_error = chunk_max;
+            const size_t row = j * nx;
+            for (size_t i = 1; i < simd_end; ++i) {
+                float nv = jac_point(pp, rhs, row + i, nx, dx_sq, dy_sq, denom, jacobi_omega, om1);
+                ppn[row + i] = nv;
+                float e = fabsf(nv - pp[row + i]);
+                colmax[i] = e > colmax[i] ? e : colmax[i];
             }
+            for (size_t i = simd_end; i < nx; ++i)   /* scalar tail, no residual */
+                ppn[row + i] = jac_point(pp, rhs, row + i, nx, dx_sq, dy_sq, denom, jacobi_omega, om1);
         }
+        max_error = 0.0f;
+        for (size_t i = 1; i < simd_end; ++i) max_error = colmax[i] > max_error ? colmax[i] : max_error;
         /* std::mem::swap (model.rs:805) */
-        m->f[ORC_PP] = ppn;
-        m->f[ORC_PPN] = pp;
-        pp = m->f[ORC_PP];
+        float *tmp = m->f[ORC_PP];
+        m->f[ORC_PP] = m->f[ORC_PPN];
+        m->f[ORC_PPN] = tmp;
+        float *p = m->f[ORC_PP];
         /* p' boundary conditions, in the reference's order (model.rs:807-815) */
         for (size_t i = 0; i < nx; ++i) {
-            pp[i] = pp[i + nx];
-            pp[i + (ny - 1) * nx] = pp[i + (ny - 2) * nx];
+            p[i] = p[i + nx];
+            p[i + (ny - 1) * nx] = p[i + (ny - 2) * nx];
         }
         for (size_t j = 0; j < ny; ++j) {
-            pp[j * nx] = pp[1 + j * nx];
-            pp[(nx - 1) + j * nx] = 0.0f;
+            p[j * nx] = p[1 + j * nx];
+            p[(nx - 1) + j * nx] = 0.0f;
         }
         m->sweeps_total++;
         if (m->tol_enabled && max_error < m->p_tol) break; /* :816 */
     }
+    free(colmax);
     m->last_pressure_residual = max_error;
     return max_error;
 }

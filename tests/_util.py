@@ -1,0 +1,26 @@
+"""Shared helpers for the test-suite (test infrastructure only)."""
+import numpy as np
+
+STATE_FIELDS = ("u", "v", "p", "u_star", "v_star", "p_prime")
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def assert_bitwise(name, got, want):
+    g, w = bits(got), bits(want)
+    assert g.shape == w.shape, f"{name}: shape {g.shape} != {w.shape}"
+    bad = np.nonzero(g != w)[0]
+    if bad.size:
+        k = bad[0]
+        raise AssertionError(
+            f"{name}: {bad.size}/{g.size} words differ; first at {k}: got "
+            f"{np.float32(got.ravel()[k])!r} want {np.float32(want.ravel()[k])!r}")
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    n = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / (n if n > 0 else 1.0))
