@@ -19,6 +19,7 @@
 
 #include "../../include/cfd.h"
 #include "cfd_internal.h"
+#include "slab_plan.h"
 
 using namespace cfd;
 
@@ -48,14 +49,6 @@ int fail(int code, const std::string &msg) {
 const float kNaN = std::nanf("");
 
 size_t round4(size_t n) { return (n + 3) & ~size_t(3); }
-
-// Rows [j0, j1) of rank `rank` in an even 1D row-slab split of ny rows.
-void slab_rows(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1) {
-    const uint64_t base = ny / (uint64_t)n_ranks, rem = ny % (uint64_t)n_ranks;
-    const uint64_t r = (uint64_t)rank;
-    *j0 = r * base + (r < rem ? r : rem);
-    *j1 = *j0 + base + (r < rem ? 1 : 0);
-}
 
 }  // namespace
 
@@ -103,51 +96,38 @@ struct cfd_model {
     }
 
     // ---------------------------------------------------------------- halos
-    // u/v ghost rows before the predictors: 2 rows of u and
-    // v each way.  v row nyl is the face shared with the rank above and is
-    // computed redundantly by both ranks, so it is not exchanged.
-    int exchange_uv() {
+    // Ghost-row exchange of one field with both neighbours (geometry from
+    // plan_halo): one RCCL group of at most two sends and two receives.
+    int exchange(float *base, size_t pitch, int kind, int depth) {
         if (!sharded()) return 0;
-        const size_t W = (size_t)g.nx + 1, nx = (size_t)g.nx;
-        const int nyl = g.nyl;
+        int h[6];
+        plan_halo(kind, g.nyl, depth, rank, n_ranks, h);
         RCCL_TRY(ncclGroupStart());
-        if (rank > 0) {
-            const int lo = rank - 1;
-            RCCL_TRY(ncclSend(f.u, 2 * W, ncclFloat, lo, comm, stream));
-            RCCL_TRY(ncclSend(f.v + nx, 2 * nx, ncclFloat, lo, comm, stream));
-            RCCL_TRY(ncclRecv(f.u - 2 * W, 2 * W, ncclFloat, lo, comm, stream));
-            RCCL_TRY(ncclRecv(f.v - 2 * nx, 2 * nx, ncclFloat, lo, comm, stream));
+        if (h[2] > 0) {
+            RCCL_TRY(ncclSend(base + (long)h[0] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
+                              rank - 1, comm, stream));
+            RCCL_TRY(ncclRecv(base + (long)h[1] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
+                              rank - 1, comm, stream));
         }
-        if (rank + 1 < n_ranks) {
-            const int hi = rank + 1;
-            RCCL_TRY(ncclSend(f.u + (size_t)(nyl - 2) * W, 2 * W, ncclFloat, hi, comm, stream));
-            RCCL_TRY(ncclSend(f.v + (size_t)(nyl - 2) * nx, 2 * nx, ncclFloat, hi, comm, stream));
-            RCCL_TRY(ncclRecv(f.u + (size_t)nyl * W, 2 * W, ncclFloat, hi, comm, stream));
-            RCCL_TRY(ncclRecv(f.v + (size_t)(nyl + 1) * nx, 2 * nx, ncclFloat, hi, comm, stream));
+        if (h[5] > 0) {
+            RCCL_TRY(ncclSend(base + (long)h[3] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
+                              rank + 1, comm, stream));
+            RCCL_TRY(ncclRecv(base + (long)h[4] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
+                              rank + 1, comm, stream));
         }
         RCCL_TRY(ncclGroupEnd());
         return 0;
     }
 
-    // p' halo: `rows` owned boundary rows of buffer `buf` each way.
-    int exchange_pp(int buf, int rows) {
-        if (!sharded()) return 0;
-        const size_t nx = (size_t)g.nx;
-        float *b = f.pp[buf];
-        const int nyl = g.nyl;
-        RCCL_TRY(ncclGroupStart());
-        if (rank > 0) {
-            RCCL_TRY(ncclSend(b, rows * nx, ncclFloat, rank - 1, comm, stream));
-            RCCL_TRY(ncclRecv(b - (size_t)rows * nx, rows * nx, ncclFloat, rank - 1, comm, stream));
-        }
-        if (rank + 1 < n_ranks) {
-            RCCL_TRY(ncclSend(b + (size_t)(nyl - rows) * nx, rows * nx, ncclFloat, rank + 1, comm,
-                              stream));
-            RCCL_TRY(ncclRecv(b + (size_t)nyl * nx, rows * nx, ncclFloat, rank + 1, comm, stream));
-        }
-        RCCL_TRY(ncclGroupEnd());
-        return 0;
+    // u/v ghost rows before the predictors.
+    int exchange_uv() {
+        int rc = exchange(f.u, (size_t)g.nx + 1, HALO_U, 2);
+        if (rc) return rc;
+        return exchange(f.v, (size_t)g.nx, HALO_V, 2);
     }
+
+    // p' halo: `rows` owned boundary rows of buffer `buf` each way.
+    int exchange_pp(int buf, int rows) { return exchange(f.pp[buf], (size_t)g.nx, HALO_PP, rows); }
 
     int allreduce_max_u32(uint32_t *dev, size_t n) {
         if (!sharded()) return 0;
@@ -176,15 +156,12 @@ struct cfd_model {
                 launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
         } else {
-            const int hg = g.hg;
             for (int it = 0; it < iters; ++it) {
-                const int s = it % hg;
-                const int ext = hg - 1 - s;
-                const int lo = std::max(-ext, lo_g);
-                const int hi = std::min(g.nyl + ext, hi_g);
+                int lo, hi, exch;
+                plan_sweep(g.j0, g.nyl, g.ny, g.hg, it, iters, &lo, &hi, &exch);
                 launch_jacobi_sweep(g, f, pass, it, lo, hi, stream);
-                if (s == hg - 1 || it == iters - 1) {
-                    int rc = exchange_pp((host_cur + it + 1) & 1, hg);
+                if (exch) {
+                    int rc = exchange_pp((host_cur + it + 1) & 1, g.hg);
                     if (rc) return rc;
                 }
             }
@@ -493,7 +470,7 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     cfd_model *m = new cfd_model();
     m->n_ranks = n_ranks;
     m->rank = rank;
-    slab_rows(grid->ny, n_ranks, rank, &m->j0, &m->j1);
+    plan_slab(grid->ny, n_ranks, rank, &m->j0, &m->j1);
     int hg = 1;
     if (n_ranks > 1) {
         const char *env = getenv("CFD_HALO_DEPTH");
@@ -826,6 +803,27 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
 }
 
 int cfd_get_halo_depth(const cfd_model *m) { return m ? m->g.hg : 0; }
+
+// ---- host-only slab plan (no device needed) ----
+int cfd_plan_slab(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1) {
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks || !j0 || !j1)
+        return fail(CFD_EINVAL, "bad plan_slab arguments");
+    plan_slab(ny, n_ranks, rank, j0, j1);
+    return 0;
+}
+
+int cfd_plan_sweep(int j0, int nyl, int ny, int halo_depth, int it, int iters, int *lo, int *hi,
+                   int *exchange) {
+    if (halo_depth < 1 || !lo || !hi || !exchange) return fail(CFD_EINVAL, "bad plan_sweep arguments");
+    plan_sweep(j0, nyl, ny, halo_depth, it, iters, lo, hi, exchange);
+    return 0;
+}
+
+int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6) {
+    if (kind < 0 || kind > 2 || !out6) return fail(CFD_EINVAL, "bad plan_halo arguments");
+    plan_halo(kind, nyl, depth, rank, n_ranks, out6);
+    return 0;
+}
 
 void cfd_destroy(cfd_model *m) {
     if (!m) return;

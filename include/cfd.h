@@ -171,6 +171,20 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
 /* p' halo depth (rows exchanged per RCCL round) of a sharded model. */
 int cfd_get_halo_depth(const cfd_model *m);
 
+/* Host-only slab plan used by cfd_create_sharded (no device needed; the
+ * multi-rank CPU tests drive the same plan):
+ *   cfd_plan_slab  — global pressure rows [j0, j1) of `rank`;
+ *   cfd_plan_sweep — local rows [lo, hi) that sweep `it` of an `iters`-sweep
+ *                    solve recomputes with halo depth d, and whether d rows
+ *                    of p' are exchanged after it;
+ *   cfd_plan_halo  — ghost geometry of a field (kind 0 u, 1 v, 2 p'):
+ *                    out6 = {send, recv, rows} with rank-1, then with rank+1,
+ *                    in local rows. */
+int cfd_plan_slab(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1);
+int cfd_plan_sweep(int j0, int nyl, int ny, int halo_depth, int it, int iters, int *lo, int *hi,
+                   int *exchange);
+int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6);
+
 const char *cfd_last_error(void);
 int cfd_abi_version(void);
 void cfd_destroy(cfd_model *m);
