@@ -21,7 +21,7 @@ import enum
 import queue
 import threading
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import List, Optional
 
 import numpy as np
@@ -32,7 +32,7 @@ from ._lib import CfdError, CfdGrid, CfdParams, CfdResiduals, CfdState, check, l
 __all__ = [
     "VelocityScheme", "InletProfile", "PressureSolver", "BoundaryKind", "Cylinder", "Grid",
     "SimulationParams", "Residuals", "SimSnapshot", "Model", "SimulationControlHandle",
-    "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "load",
+    "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "load", "LocalHub",
 ]
 
 
@@ -147,6 +147,20 @@ class SimSnapshot:                           # model.rs:36-42
     paused: bool = False
 
 
+class LocalHub:
+    """In-process stand-in for the RCCL communicator (testing): slabs of one
+    grid driven by threads of this process (cfd_local_hub_create)."""
+
+    def __init__(self, n_ranks: int):
+        self.handle = load().cfd_local_hub_create(n_ranks)
+        self.n_ranks = n_ranks
+
+    def close(self):
+        if self.handle:
+            load().cfd_local_hub_destroy(self.handle)
+            self.handle = None
+
+
 def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     check("cfd_rccl_unique_id", load().cfd_rccl_unique_id(buf))
@@ -164,7 +178,8 @@ class Model:
     """`Model` (model.rs:166-214) with its fields resident in HBM."""
 
     def __init__(self, grid: Grid, params: SimulationParams, device: int = 0, *,
-                 n_ranks: int = 1, rank: int = 0, unique_id: Optional[bytes] = None):
+                 n_ranks: int = 1, rank: int = 0, unique_id: Optional[bytes] = None,
+                 local_hub: Optional["LocalHub"] = None):
         L = load()
         self.grid = grid
         self.params = params
@@ -172,6 +187,10 @@ class Model:
         g, p = grid._c(), params._c()
         if n_ranks == 1:
             check("cfd_create", L.cfd_create(C.byref(g), C.byref(p), device, C.byref(self._h)))
+        elif local_hub is not None:
+            check("cfd_create_sharded_local",
+                  L.cfd_create_sharded_local(C.byref(g), C.byref(p), device, n_ranks, rank,
+                                             local_hub.handle, C.byref(self._h)))
         else:
             check("cfd_create_sharded",
                   L.cfd_create_sharded(C.byref(g), C.byref(p), device, n_ranks, rank,

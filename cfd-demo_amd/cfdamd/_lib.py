@@ -13,7 +13,8 @@ LIB_PATH = os.path.join(ROOT, "lib", "libcfd_amd.so")
 # Every entry point include/cfd.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "cfd_default_params", "cfd_default_grid", "cfd_create", "cfd_rccl_unique_id",
-    "cfd_create_sharded", "cfd_get_slab", "cfd_update", "cfd_update_n", "cfd_piso_step",
+    "cfd_create_sharded", "cfd_local_hub_create", "cfd_local_hub_destroy",
+    "cfd_create_sharded_local", "cfd_get_slab", "cfd_update", "cfd_update_n", "cfd_piso_step",
     "cfd_pressure_solve", "cfd_run_phase", "cfd_set_params", "cfd_get_snapshot",
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
@@ -81,6 +82,10 @@ def load():
         "cfd_rccl_unique_id": (i32, [C.c_char_p]),
         "cfd_create_sharded": (i32, [C.POINTER(CfdGrid), C.POINTER(CfdParams), i32, i32, i32,
                                      C.c_char_p, C.POINTER(vp)]),
+        "cfd_local_hub_create": (vp, [i32]),
+        "cfd_local_hub_destroy": (None, [vp]),
+        "cfd_create_sharded_local": (i32, [C.POINTER(CfdGrid), C.POINTER(CfdParams), i32, i32,
+                                           i32, vp, C.POINTER(vp)]),
         "cfd_get_slab": (i32, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "cfd_update": (i32, [vp]),
         "cfd_update_n": (i32, [vp, i32]),

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     const __amdgpu_buffer_rsrc_t rs_p =
         __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs_r =
-        __builtin_amdgcn_make_buffer_rsrc((void *)rhs, 0, nyl * nx * 4, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)hg * nx), 0, pbytes, 0x00020000);
     float *__restrict__ dst = dst_alloc + (long)hg * nx;
 
     const float dx = g.dx, dy = g.dy;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     const int row_bytes = nx * 4;
     // byte offsets at local row 0 (p' offsets include the hg ghost rows)
     const int off_p = valid ? (hg * nx + col) * 4 : kOOB;
-    const int off_r = valid ? col * 4 : kOOB;
+    const int off_r = valid ? (hg * nx + col) * 4 : kOOB;
     const int off_l = (lane == 0 && ch > 0 && valid) ? (hg * nx + col - 1) * 4 : kOOB;
     const int off_rt = (lane == 63 && ch + 1 < nch) ? (hg * nx + col + 4) * 4 : kOOB;
     const bool e0 = (col >= 1) && (col <= nx - 8);   // residual columns 1..=nx-8

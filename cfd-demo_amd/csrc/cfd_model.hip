@@ -12,6 +12,8 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -50,6 +52,36 @@ const float kNaN = std::nanf("");
 
 size_t round4(size_t n) { return (n + 3) & ~size_t(3); }
 
+// In-process stand-in for the RCCL communicator (testing only): n slabs in
+// one process, each driven by its own host thread, possibly all on one GPU.
+// Halo exchanges become device-to-device copies between the members' buffers
+// and the max all-reduce a host fold, each fenced by host barriers.  Every
+// kernel and every row range the sharded path launches is unchanged, so a
+// 1-GPU box can check the whole decomposition against the single-domain
+// oracle (tests/test_gpu_sharded.py).
+struct LocalHub {
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<cfd_model *> members;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t my = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != my; });
+        }
+    }
+};
+
+// Fields that travel between slabs.
+enum FieldId { FLD_U = 0, FLD_V, FLD_PP0, FLD_PP1, FLD_RHS };
+
 }  // namespace
 
 struct cfd_model {
@@ -71,6 +103,7 @@ struct cfd_model {
     int n_ranks = 1, rank = 0;
     uint64_t j0 = 0, j1 = 0;
     ncclComm_t comm = nullptr;
+    LocalHub *hub = nullptr;   // testing stand-in for comm
     int host_cur = 0;   // mirror of ctl->cur, valid when the tolerance is off
     // timing
     hipEvent_t ev_step0 = nullptr, ev_step1 = nullptr, ev_prof0 = nullptr, ev_prof1 = nullptr;
@@ -96,10 +129,24 @@ struct cfd_model {
     }
 
     // ---------------------------------------------------------------- halos
+    float *field_ptr(int id) {
+        switch (id) {
+        case FLD_U: return f.u;
+        case FLD_V: return f.v;
+        case FLD_PP0: return f.pp[0];
+        case FLD_PP1: return f.pp[1];
+        default: return f.rhs;
+        }
+    }
+    size_t field_pitch(int id) const { return id == FLD_U ? (size_t)g.nx + 1 : (size_t)g.nx; }
+
     // Ghost-row exchange of one field with both neighbours (geometry from
     // plan_halo): one RCCL group of at most two sends and two receives.
-    int exchange(float *base, size_t pitch, int kind, int depth) {
+    int exchange(int id, int kind, int depth) {
         if (!sharded()) return 0;
+        if (hub) return exchange_local(id, kind, depth);
+        float *base = field_ptr(id);
+        const size_t pitch = field_pitch(id);
         int h[6];
         plan_halo(kind, g.nyl, depth, rank, n_ranks, h);
         RCCL_TRY(ncclGroupStart());
@@ -119,18 +166,56 @@ struct cfd_model {
         return 0;
     }
 
+    // LocalHub form: copy the neighbours' send rows straight into our ghosts.
+    int exchange_local(int id, int kind, int depth) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        hub->barrier();   // every member's rows are final
+        float *base = field_ptr(id);
+        const size_t pitch = field_pitch(id);
+        int h[6];
+        plan_halo(kind, g.nyl, depth, rank, n_ranks, h);
+        for (int side = 0; side < 2; ++side) {
+            const int rows = h[3 * side + 2];
+            if (rows == 0) continue;
+            cfd_model *peer = hub->members[side == 0 ? rank - 1 : rank + 1];
+            int ph[6];
+            plan_halo(kind, peer->g.nyl, depth, peer->rank, n_ranks, ph);
+            const int psend = side == 0 ? ph[3] : ph[0];   // peer's rows facing us
+            HIP_TRY(hipMemcpyAsync(base + (long)h[3 * side + 1] * (long)pitch,
+                                   peer->field_ptr(id) + (long)psend * (long)pitch,
+                                   (size_t)rows * pitch * 4, hipMemcpyDeviceToDevice, stream));
+        }
+        HIP_TRY(hipStreamSynchronize(stream));
+        hub->barrier();   // nobody overwrites rows a peer is still copying
+        return 0;
+    }
+
     // u/v ghost rows before the predictors.
     int exchange_uv() {
-        int rc = exchange(f.u, (size_t)g.nx + 1, HALO_U, 2);
+        int rc = exchange(FLD_U, HALO_U, 2);
         if (rc) return rc;
-        return exchange(f.v, (size_t)g.nx, HALO_V, 2);
+        return exchange(FLD_V, HALO_V, 2);
     }
 
     // p' halo: `rows` owned boundary rows of buffer `buf` each way.
-    int exchange_pp(int buf, int rows) { return exchange(f.pp[buf], (size_t)g.nx, HALO_PP, rows); }
+    int exchange_pp(int buf, int rows) { return exchange(buf ? FLD_PP1 : FLD_PP0, HALO_PP, rows); }
 
     int allreduce_max_u32(uint32_t *dev, size_t n) {
         if (!sharded()) return 0;
+        if (hub) {
+            std::vector<uint32_t> acc(n, 0u), mine(n);
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();
+            const size_t off = (size_t)(dev - (uint32_t *)f.ctl);   // same slot in every member
+            for (cfd_model *peer : hub->members) {
+                HIP_TRY(hipMemcpy(mine.data(), (uint32_t *)peer->f.ctl + off, n * 4,
+                                  hipMemcpyDeviceToHost));
+                for (size_t k = 0; k < n; ++k) acc[k] = std::max(acc[k], mine[k]);
+            }
+            hub->barrier();
+            HIP_TRY(hipMemcpy(dev, acc.data(), n * 4, hipMemcpyHostToDevice));
+            return 0;
+        }
         RCCL_TRY(ncclAllReduce(dev, dev, n, ncclUint32, ncclMax, comm, stream));
         return 0;
     }
@@ -156,6 +241,9 @@ struct cfd_model {
                 launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
         } else {
+            // the deep-halo sweeps recompute ghost rows, which read rhs there
+            int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
+            if (rc0) return rc0;
             for (int it = 0; it < iters; ++it) {
                 int lo, hi, exch;
                 plan_sweep(g.j0, g.nyl, g.ny, g.hg, it, iters, &lo, &hi, &exch);
@@ -380,7 +468,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     if ((rc = zalloc((void **)&m->u_all, u_alloc * 4)) || (rc = zalloc((void **)&m->v_all, v_alloc * 4)) ||
         (rc = zalloc((void **)&m->uo_all, u_alloc * 4)) || (rc = zalloc((void **)&m->vo_all, v_alloc * 4)) ||
         (rc = zalloc((void **)&m->us_all, u_alloc * 4)) || (rc = zalloc((void **)&m->vs_all, v_alloc * 4)) ||
-        (rc = zalloc((void **)&m->p, p_n * 4)) || (rc = zalloc((void **)&m->rhs, p_n * 4)) ||
+        (rc = zalloc((void **)&m->p, p_n * 4)) || (rc = zalloc((void **)&m->rhs, pp_n * 4)) ||
         (rc = zalloc((void **)&m->pp_all[0], pp_n * 4)) || (rc = zalloc((void **)&m->pp_all[1], pp_n * 4)) ||
         (rc = zalloc((void **)&m->mask_u, nyl * W + 16)) || (rc = zalloc((void **)&m->mask_v, (nyl + 1) * nx + 16)) ||
         (rc = zalloc((void **)&m->ctl, sizeof(Ctl))))
@@ -438,7 +526,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.u_star = m->us_all + uoff;
     f.v_star = m->vs_all + voff;
     f.p = m->p;
-    f.rhs = m->rhs;
+    f.rhs = m->rhs + (size_t)hg * nx;   // hg ghost rows each side (sharded solves)
     f.pp[0] = m->pp_all[0] + (size_t)hg * nx;
     f.pp[1] = m->pp_all[1] + (size_t)hg * nx;
     f.mask_u = m->mask_u;
@@ -457,7 +545,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
 }
 
 int create_common(const cfd_grid *grid, const cfd_params *params, int device, int n_ranks, int rank,
-                  const void *uid, cfd_model **out) {
+                  const void *uid, LocalHub *hub, cfd_model **out) {
     if (!out) return fail(CFD_EINVAL, "null out");
     *out = nullptr;
     int rc = validate(grid, params);
@@ -484,7 +572,15 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
         }
     }
     rc = build_model(m, grid, params, device, hg);
-    if (!rc && n_ranks > 1) {
+    if (!rc && n_ranks > 1 && hub) {
+        if (hub->n != n_ranks) {
+            rc = fail(CFD_EINVAL, "local hub size != n_ranks");
+        } else {
+            std::lock_guard<std::mutex> lk(hub->mu);
+            hub->members[rank] = m;
+            m->hub = hub;
+        }
+    } else if (!rc && n_ranks > 1) {
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, id, rank);
@@ -536,7 +632,7 @@ void cfd_default_grid(cfd_grid *o) {
 }
 
 int cfd_create(const cfd_grid *grid, const cfd_params *params, int device_ordinal, cfd_model **out) {
-    return create_common(grid, params, device_ordinal, 1, 0, nullptr, out);
+    return create_common(grid, params, device_ordinal, 1, 0, nullptr, nullptr, out);
 }
 
 int cfd_rccl_unique_id(void *out) {
@@ -551,7 +647,24 @@ int cfd_rccl_unique_id(void *out) {
 int cfd_create_sharded(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
                        int n_ranks, int rank, const void *uid, cfd_model **out) {
     if (n_ranks > 1 && !uid) return fail(CFD_EINVAL, "null rccl unique id");
-    return create_common(grid, params, device_ordinal, n_ranks, rank, uid, out);
+    return create_common(grid, params, device_ordinal, n_ranks, rank, uid, nullptr, out);
+}
+
+void *cfd_local_hub_create(int n_ranks) {
+    if (n_ranks < 1) return nullptr;
+    LocalHub *h = new LocalHub();
+    h->n = n_ranks;
+    h->members.assign(n_ranks, nullptr);
+    return h;
+}
+
+void cfd_local_hub_destroy(void *hub) { delete static_cast<LocalHub *>(hub); }
+
+int cfd_create_sharded_local(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
+                             int n_ranks, int rank, void *hub, cfd_model **out) {
+    if (!hub) return fail(CFD_EINVAL, "null local hub");
+    return create_common(grid, params, device_ordinal, n_ranks, rank, nullptr,
+                         static_cast<LocalHub *>(hub), out);
 }
 
 int cfd_get_slab(const cfd_model *m, uint64_t *j0, uint64_t *j1) {

@@ -119,6 +119,15 @@ int cfd_create(const cfd_grid *grid, const cfd_params *params, int device_ordina
 int cfd_rccl_unique_id(void *out_128_bytes);
 int cfd_create_sharded(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
                        int n_ranks, int rank, const void *rccl_unique_id, cfd_model **out);
+/* Testing stand-in for the RCCL communicator: n_ranks slabs inside ONE
+ * process (one host thread per slab, any devices, several may share a GPU);
+ * halo exchanges become device-to-device copies between the members and the
+ * max all-reduce a host fold.  Kernels and row plans are those of the RCCL
+ * path; only the transport differs.  Destroy the hub after its members. */
+void *cfd_local_hub_create(int n_ranks);
+void cfd_local_hub_destroy(void *hub);
+int cfd_create_sharded_local(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
+                             int n_ranks, int rank, void *hub, cfd_model **out);
 /* Global pressure rows [j0, j1) held by this model (0, ny for cfd_create). */
 int cfd_get_slab(const cfd_model *m, uint64_t *j0, uint64_t *j1);
 

@@ -1,0 +1,121 @@
+"""GPU: the row-slab decomposition (cfd_create_sharded's kernels, row plans,
+ghost layouts and deep-halo sweeps) against the single-domain oracle, bit for
+bit, on ONE device.  The slabs live in one process and talk through the
+in-process LocalHub transport (cfd_create_sharded_local) instead of RCCL —
+RCCL refuses two ranks on one GPU — so everything but the RCCL calls
+themselves is exercised here; bench.py drives the RCCL transport on N GPUs."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from _util import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def run_sharded(n, grid, params, steps, halo_depth):
+    import cfdamd
+    os.environ["CFD_HALO_DEPTH"] = str(halo_depth)
+    hub = cfdamd.LocalHub(n)
+    states, models, errors = [None] * n, [None] * n, []
+
+    def worker(r):
+        try:
+            m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=r, local_hub=hub)
+            models[r] = m
+            for _ in range(steps):
+                m.update()
+            m.synchronize()
+            states[r] = (m.j0, m.j1, m.get_state(), m.halo_depth)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    for m in models:
+        if m is not None:
+            m.close()
+    hub.close()
+    os.environ.pop("CFD_HALO_DEPTH", None)
+    if errors:
+        raise errors[0]
+    return states
+
+
+def assemble(states, nx):
+    """Owned rows of every slab -> global flat arrays (v gets the top face
+    from the last slab)."""
+    out = {}
+    for f in ("u", "p", "p_prime", "u_star", "rhs"):
+        out[f] = np.concatenate([s[f] for (_, _, s, _) in states])
+    for f in ("v", "v_star"):
+        parts = []
+        for k, (j0, j1, s, _) in enumerate(states):
+            rows = s[f].reshape(j1 - j0 + 1, nx)
+            parts.append(rows if k == len(states) - 1 else rows[:-1])
+            if k < len(states) - 1:
+                # the shared face row is held (and computed) by both ranks
+                nxt = states[k + 1][2][f].reshape(-1, nx)[0]
+                assert_bitwise(f"{f} shared face row {j1}", rows[-1], nxt)
+        out[f] = np.concatenate(parts).ravel()
+    return out
+
+
+def check_against_oracle(states, grid, oracle_kw, steps, fields):
+    from oracle import OracleModel
+    c = grid.obstacle
+    o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly,
+                    cylinder=(c.center_x, c.center_y, c.radius) if c else None, **oracle_kw)
+    for _ in range(steps):
+        o.update()
+    got = assemble(states, grid.nx)
+    for f in fields:
+        assert_bitwise(f, got[f], o.field(f))
+    s = o.scalars()
+    for (_, _, st, _) in states:
+        assert np.float32(st["dt"]) == np.float32(s.dt)
+        assert np.float32(st["last_p_residual"]) == np.float32(s.p)
+        assert np.float32(st["last_u_residual"]) == np.float32(s.u)
+        assert st["simulation_step"] == s.step
+
+
+FIELDS = ("u", "v", "p", "p_prime", "u_star", "v_star")
+
+
+@pytest.mark.parametrize("n,depth", [(2, 1), (3, 3), (4, 8), (2, 5)])
+def test_sharded_fixed_mode_cavity(n, depth):
+    import cfdamd
+    grid = cfdamd.cavity_grid(64, 96)
+    params = cfdamd.SimulationParams.cavity(100.0, 30, corrector_passes=2, tol_enabled=False)
+    st = run_sharded(n, grid, params, 5, depth)
+    assert all(s[3] == min(depth, 96 // n - 2) for s in st)
+    check_against_oracle(st, grid, dict(bc_kind=1, viscosity=0.01, jacobi_iters=30,
+                                        corrector_passes=2, tol_enabled=0), 5, FIELDS)
+
+
+@pytest.mark.parametrize("n,scheme", [(2, 1), (3, 0)])
+def test_sharded_parity_mode_channel_cylinder_across_slabs(n, scheme):
+    """Reference defaults (tolerance on, 20 corrector passes): host-driven
+    early exits with an all-reduced residual every sweep; the cylinder
+    straddles the slab boundary."""
+    import cfdamd
+    grid = cfdamd.Grid(128, 60, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.9))
+    params = cfdamd.SimulationParams(velocity_scheme=cfdamd.VelocityScheme(scheme))
+    st = run_sharded(n, grid, params, 4, 8)
+    check_against_oracle(st, grid, dict(scheme=scheme), 4, FIELDS)
+
+
+def test_sharded_bench_like_config():
+    """The bench's timed mode (200 sweeps, tolerance off, no extra passes) with
+    the default halo depth 8, four slabs."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(256, 256)
+    params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
+    st = run_sharded(4, grid, params, 3, 8)
+    check_against_oracle(st, grid, dict(bc_kind=1, viscosity=0.001, jacobi_iters=200,
+                                        corrector_passes=0, tol_enabled=0), 3, FIELDS)

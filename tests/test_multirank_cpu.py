@@ -1,0 +1,207 @@
+"""CPU, multi-process (gloo, world size 2 and 3): the 1D row-slab plan that
+cfd_create_sharded drives on the GPUs (cfd-demo_amd/csrc/slab_plan.h, through
+the C ABI cfd_plan_*) reproduces the single-domain result bit for bit.
+
+Each rank holds its slab with ghost rows, runs Jacobi sweeps over exactly the
+rows cfd_plan_sweep names (a numpy emulation of k_jacobi's arithmetic and
+fused p' boundary stores), exchanges exactly the rows cfd_plan_halo names via
+torch.distributed send/recv, and the gathered result must equal the
+single-domain oracle (oracle/cfd_oracle.c) word for word.  The exchange
+geometry of u and v is checked by shipping global row ids.
+"""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+F = np.float32
+
+
+def _lib():
+    import sys
+    for p in (os.path.join(ROOT, "cfd-demo_amd"), os.path.join(ROOT, "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from cfdamd import _lib as L
+    return L.load()
+
+
+def plan_slab(ny, n, r):
+    a, b = C.c_uint64(), C.c_uint64()
+    assert _lib().cfd_plan_slab(ny, n, r, C.byref(a), C.byref(b)) == 0
+    return int(a.value), int(b.value)
+
+
+def plan_sweep(j0, nyl, ny, hg, it, iters):
+    lo, hi, ex = C.c_int(), C.c_int(), C.c_int()
+    assert _lib().cfd_plan_sweep(j0, nyl, ny, hg, it, iters, C.byref(lo), C.byref(hi),
+                                 C.byref(ex)) == 0
+    return lo.value, hi.value, bool(ex.value)
+
+
+def plan_halo(kind, nyl, depth, r, n):
+    out = (C.c_int * 6)()
+    assert _lib().cfd_plan_halo(kind, nyl, depth, r, n, out) == 0
+    return list(out)
+
+
+def sweep_rows(src, dst, rhs, g0, lo, hi, nx, ny, j0, dx, dy):
+    """k_jacobi on local rows [lo, hi); src, dst and rhs all carry g0 ghost
+    rows in front (rhs ghosts are exchanged once per solve)."""
+    omega, om1 = F(0.75), F(1.0) - F(0.75)
+    dx2, dy2 = dx * dx, dy * dy
+    denom = F(2.0) / (dx * dx) + F(2.0) / (dy * dy)
+    for lj in range(lo, hi):
+        r = lj + g0
+        Cc, T, B = src[r], src[r + 1], src[r - 1]
+        L = np.concatenate(([F(0)], Cc[:-1]))
+        R = np.concatenate((Cc[1:], [F(0)]))
+        h = (R + L) / dx2
+        v = (T + B) / dy2
+        n = omega * ((h + v - rhs[r]) / denom) + om1 * Cc
+        n[0] = n[1]
+        n[nx - 1] = F(0)
+        dst[r] = n
+        if j0 + lj == 1:
+            dst[r - 1] = n
+        if j0 + lj == ny - 2:
+            dst[r + 1] = n
+
+
+def exchange(arr, g0, spec, rank, n):
+    """arr rows indexed local+g0; spec = cfd_plan_halo output."""
+    reqs = []
+    for peer, (s, rcv, rows) in ((rank - 1, spec[0:3]), (rank + 1, spec[3:6])):
+        if rows == 0:
+            continue
+        buf = torch.from_numpy(np.ascontiguousarray(arr[s + g0:s + g0 + rows]))
+        reqs.append(dist.isend(buf, peer))
+    for peer, (s, rcv, rows) in ((rank - 1, spec[0:3]), (rank + 1, spec[3:6])):
+        if rows == 0:
+            continue
+        buf = torch.empty((rows, arr.shape[1]), dtype=torch.float32)
+        dist.recv(buf, peer)
+        arr[rcv + g0:rcv + g0 + rows] = buf.numpy()
+    for q in reqs:
+        q.wait()
+
+
+def _worker(rank, n, port, cases, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    try:
+        out = []
+        for (nx, ny, hg, iters, seed) in cases:
+            rng = np.random.default_rng(seed)
+            P = rng.uniform(-1, 1, (ny, nx)).astype(F)
+            RHS = rng.uniform(-1, 1, (ny, nx)).astype(F)
+            dx, dy = F(F(2.0) / F(nx)), F(F(1.0) / F(ny))
+            j0, j1 = plan_slab(ny, n, rank)
+            nyl = j1 - j0
+            g0 = hg
+            bufs = [np.zeros((nyl + 2 * hg, nx), F) for _ in range(2)]
+            rhs = np.zeros((nyl + 2 * hg, nx), F)
+            # owned rows only, then the ghost exchanges the GPU path performs:
+            # p' (end of the previous solve / cfd_set_state) and rhs (solve start)
+            bufs[0][g0:g0 + nyl] = P[j0:j1]
+            rhs[g0:g0 + nyl] = RHS[j0:j1]
+            exchange(bufs[0], g0, plan_halo(2, nyl, hg, rank, n), rank, n)
+            exchange(rhs, g0, plan_halo(2, nyl, hg, rank, n), rank, n)
+            cur = 0
+            for it in range(iters):
+                lo, hi, ex = plan_sweep(j0, nyl, ny, hg, it, iters)
+                sweep_rows(bufs[cur], bufs[cur ^ 1], rhs, g0, lo, hi, nx, ny, j0, dx, dy)
+                cur ^= 1
+                if ex:
+                    exchange(bufs[cur], g0, plan_halo(2, nyl, hg, rank, n), rank, n)
+            mine = torch.from_numpy(np.ascontiguousarray(bufs[cur][g0:g0 + nyl]))
+            if rank == 0:
+                parts = [mine.numpy()]
+                for r in range(1, n):
+                    a, b = plan_slab(ny, n, r)
+                    t = torch.empty((b - a, nx), dtype=torch.float32)
+                    dist.recv(t, r)
+                    parts.append(t.numpy())
+                out.append(np.concatenate(parts).ravel())
+            else:
+                dist.send(mine, 0)
+            # u / v ghost geometry: ship global row ids
+            for kind, rows_owned, pitch in ((0, nyl, nx + 1), (1, nyl + 1, nx)):
+                arr = np.full((nyl + 1 + 4, pitch), -1.0, F)
+                for lj in range(rows_owned):
+                    arr[lj + 2] = j0 + lj
+                exchange(arr, 2, plan_halo(kind, nyl, 2, rank, n), rank, n)
+                want_rows = list(range(-2, 0)) if rank > 0 else []
+                if rank < n - 1:
+                    want_rows += list(range(nyl, nyl + 2)) if kind == 0 else \
+                        list(range(nyl + 1, nyl + 3))
+                for lj in want_rows:
+                    assert (arr[lj + 2] == j0 + lj).all(), (kind, rank, lj, arr[lj + 2][:3])
+        if rank == 0:
+            results.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+CASES = [  # nx, ny, halo depth, sweeps, seed
+    (16, 40, 1, 5, 1),
+    (24, 40, 3, 7, 2),
+    (32, 44, 8, 20, 3),
+    (16, 30, 4, 4, 4),
+    (16, 37, 2, 9, 5),
+]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_sharded_jacobi_plan_matches_single_domain(n):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleModel
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, n, port, CASES, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for (nx, ny, hg, iters, seed), res in zip(CASES, got):
+        rng = np.random.default_rng(seed)
+        P = rng.uniform(-1, 1, (ny, nx)).astype(F)
+        RHS = rng.uniform(-1, 1, (ny, nx)).astype(F)
+        o = OracleModel(nx, ny, 2.0, 1.0, jacobi_iters=iters, tol_enabled=0)
+        o.field("p_prime")[:] = P.ravel()
+        o.field("rhs")[:] = RHS.ravel()
+        o.jacobi()
+        want = o.field("p_prime")
+        assert np.array_equal(res.view(np.uint32), want.view(np.uint32)), (nx, ny, hg, iters)
+
+
+def test_plan_slab_partition_properties():
+    for ny in (4, 5, 37, 4096, 8192):
+        for n in (1, 2, 3, 4, 8):
+            if ny < n:
+                continue
+            rows = [plan_slab(ny, n, r) for r in range(n)]
+            assert rows[0][0] == 0 and rows[-1][1] == ny
+            assert all(rows[k][1] == rows[k + 1][0] for k in range(n - 1))
+            sizes = [b - a for a, b in rows]
+            assert max(sizes) - min(sizes) <= 1
