@@ -143,9 +143,13 @@ def main():
     finite = bool(np.isfinite(snap.u).all() and np.isfinite(snap.v).all())
 
     cells_local = nx * model.nyl
-    sweep_ms = tm["solve_ms"] / max(tm["sweeps"], 1)
-    bytes_launch = BYTES_PER_CELL_UPDATE * cells_local
-    achieved = bytes_launch / (sweep_ms * 1e-3) / 1e9 if sweep_ms > 0 else 0.0
+    kcfg = model.kernel_config
+    T = kcfg["temporal"]
+    launches = max(tm["sweeps"] // T, 1)
+    launch_ms = tm["solve_ms"] / launches
+    # algorithmic bytes per launch = 12 B/cell-update x cells x sweeps per launch
+    bytes_launch = BYTES_PER_CELL_UPDATE * cells_local * T
+    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
 
     if rank == 0:
         out = {
@@ -166,15 +170,22 @@ def main():
                             "sweeps/step, tolerance off, 0 extra corrector passes",
                 "grid": [nx, ny], "slab_per_gpu": [nx, model.nyl], "jacobi_iters": args.iters,
                 "parallelism": f"row-slab x{n}" + (f", halo depth {model.halo_depth}" if n > 1 else ""),
-                "kernel": "k_jacobi (float4 column strips, 16-row register march)",
+                "kernel": (f"k_jacobi_tb<{T}> ({T} sweeps/launch, register-march temporal "
+                           "blocking)" if T > 1 else "k_jacobi (1 sweep/launch)"),
+                "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
+                             "FMA-corrected (proven exact, 2^32 inputs)"][kcfg["fastdiv"]],
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "k_jacobi", "avg_launch_us": sweep_ms * 1e3,
+                "kernel": "k_jacobi_tb" if T > 1 else "k_jacobi", "sweeps_per_launch": T,
+                "avg_launch_us": launch_ms * 1e3,
                 "algorithmic_bytes_per_launch": bytes_launch,
-                "timing": "HIP events on the model stream around each step's sweep sequence, "
-                          "/ sweeps (includes inter-launch gaps)",
+                "timing": "HIP events on the model stream around each step's launch sequence, "
+                          "/ launches (includes inter-launch gaps)",
+                "note": "achieved counts 12 B per cell-update (SURVEY §8(d)); with T sweeps "
+                        "per launch the HBM bytes moved are ~1/T of that, so frac > 1 means "
+                        "the kernel beats the single-sweep HBM roofline by on-chip reuse",
             },
             "solve_fraction_of_step": tm["solve_ms"] / tm["step_ms"] if tm["step_ms"] else None,
             "final_step": res.simulation_step, "final_dt": res.dt, "fields_finite": finite,

@@ -322,6 +322,13 @@ class Model:
                 "steps": int(d.value)}
 
     @property
+    def kernel_config(self) -> dict:
+        fd, tb = C.c_int(), C.c_int()
+        check("cfd_get_kernel_config",
+              load().cfd_get_kernel_config(self._h, C.byref(fd), C.byref(tb)))
+        return {"fastdiv": fd.value, "temporal": tb.value}
+
+    @property
     def halo_depth(self) -> int:
         return int(load().cfd_get_halo_depth(self._h))
 

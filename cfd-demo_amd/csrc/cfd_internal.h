@@ -11,8 +11,9 @@
 //     u, u_old, u_star : rows [-G, nyl+G)        (G = 2)
 //     v, v_old, v_star : rows [-G, nyl+1+G)      (v row nyl is the face shared
 //                                                 with the rank above)
-//     p, rhs           : rows [0, nyl)
-//     p' (two buffers) : rows [-HG, nyl+HG)      (HG = halo depth >= 1)
+//     p                : rows [0, nyl)
+//     rhs, p' (x2)     : rows [-HG, nyl+HG)      (HG = halo depth >= 1; deep-halo
+//                                                 sweeps recompute ghost rows)
 //   mask_u rows [0,nyl), mask_v rows [0,nyl] (u8, same pitches).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -53,6 +54,13 @@ struct Geom {
     int32_t tol_enabled;
     float p_tol;
     int32_t jacobi_iters;
+    // Jacobi divisors exactly as model.rs:740-746 forms them, their rounded
+    // reciprocals, and the division mode proven exact for all three
+    // (0: IEEE `/`, 1: x * (1/c), 2: x * (1/c) + one FMA correction step);
+    // see verify_division() in cfd_model.hip.
+    float dx_sq, dy_sq, denom;
+    float r_dx_sq, r_dy_sq, r_denom;
+    int32_t fastdiv;
 };
 
 struct Fields {
@@ -78,6 +86,14 @@ void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_overri
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).
 void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int row_lo,
                          int row_hi, hipStream_t s);
+// T consecutive Jacobi sweeps in one launch (temporal blocking, tolerance
+// off): the final sweep's rows [out_lo, out_hi) are stored; sweep `it` of the
+// block is the first.  T <= kMaxTemporal.
+void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int T, int out_lo,
+                         int out_hi, hipStream_t s);
+// Exhaustive check over all 2^32 f32 inputs x of x/c against the two fast
+// forms; writes mismatch counts {mode1, mode2} to dev_counts (2 x u64).
+void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s);
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
                            hipStream_t s);
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
@@ -88,6 +104,8 @@ void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 
 // Jacobi kernel geometry (exported for the roofline bookkeeping in bench).
 constexpr int kJacRowsPerWave = 16;
+constexpr int kMaxTemporal = 4;     // sweeps per temporally blocked launch
+constexpr int kTbRowsPerWave = 32;  // output rows per wave segment (TB kernel)
 constexpr int kJacWavesPerBlock = 4;
 
 }  // namespace cfd

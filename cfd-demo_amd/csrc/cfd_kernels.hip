@@ -31,6 +31,48 @@ __device__ __forceinline__ float wave_max(float m) {
     return m;
 }
 
+// x / c with the reference's IEEE rounding.  FAST 1 and 2 are used only for
+// divisors whose result equals IEEE `/` for every one of the 2^32 inputs,
+// proven on the device at model creation (verify_division, cfd_model.hip).
+template <int FAST>
+__device__ __forceinline__ float fdiv(float x, float c, float r) {
+    if (FAST == 1) return x * r;
+    if (FAST == 2) {
+        const float q0 = x * r;
+        const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
+        return __builtin_isfinite(q0) ? q : q0;
+    }
+    return x / c;
+}
+
+// Exhaustive proof of the fast forms for one divisor c (r = RN(1/c)):
+// counts inputs x where x*r (mode 1) or the corrected form (mode 2) differs
+// from IEEE x/c; NaN results compare equal to NaN.
+__global__ __launch_bounds__(kBlock) void k_verify_division(float c, float r,
+                                                            unsigned long long *counts) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t bad1 = 0, bad2 = 0;
+    for (uint64_t k = tid; k < (1ull << 32); k += stride) {
+        const float x = __uint_as_float((uint32_t)k);
+        const float ref = x / c;
+        const float m1 = fdiv<1>(x, c, r);
+        const float m2 = fdiv<2>(x, c, r);
+        const bool rn = ref != ref;
+        bad1 += (rn ? (m1 == m1) : (__float_as_uint(m1) != __float_as_uint(ref))) ? 1u : 0u;
+        bad2 += (rn ? (m2 == m2) : (__float_as_uint(m2) != __float_as_uint(ref))) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        bad1 += __shfl_xor(bad1, o, 64);
+        bad2 += __shfl_xor(bad2, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (bad1) atomicAdd(&counts[0], (unsigned long long)bad1);
+        if (bad2) atomicAdd(&counts[1], (unsigned long long)bad2);
+    }
+}
+
 // ------------------------------------------------------------- copies (K0/K5b)
 
 __device__ __forceinline__ void copy4(float *__restrict__ dst, const float *__restrict__ src,
@@ -264,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pas
 // Residual: max |N - P| over columns 1..=nx-8 only (the reference's full
 // 8-lane chunks; the scalar tail :755-772 never updates max_error), owned
 // rows only, NaN-ignoring like reduce_max.  One atomicMax per wave.
-template <int R>
+template <int R, int FAST>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, int pass, int it, int row_lo, int row_hi, int nbx) {
@@ -297,12 +339,10 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
         __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)hg * nx), 0, pbytes, 0x00020000);
     float *__restrict__ dst = dst_alloc + (long)hg * nx;
 
-    const float dx = g.dx, dy = g.dy;
-    const float dx_sq = dx * dx;
-    const float dy_sq = dy * dy;
+    const float dx_sq = g.dx_sq, dy_sq = g.dy_sq, denom = g.denom;
+    const float r_dx_sq = g.r_dx_sq, r_dy_sq = g.r_dy_sq, r_denom = g.r_denom;
     const float omega = 0.75f;
     const float om1 = 1.0f - omega;
-    const float denom = 2.0f / (dx * dx) + 2.0f / (dy * dy);
 
     constexpr int kOOB = -16;   // >= num_records as unsigned: reads 0
     const int col = 4 * ch;
@@ -366,9 +406,9 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
             float n[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float horizontal = (rr[k] + ll[k]) / dx_sq;
-                const float vertical = (tt[k] + bb[k]) / dy_sq;
-                const float p_update = (horizontal + vertical - hh[k]) / denom;
+                const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
+                const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
+                const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
                 n[k] = omega * p_update + om1 * cc[k];
             }
             if (row >= 0 && row < nyl) {
@@ -397,6 +437,154 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     }
     m = wave_max(m);
     if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it], __float_as_uint(m));
+}
+
+// T weighted-Jacobi sweeps in one launch (temporal blocking; fixed-count
+// solves only — the tolerance test needs every sweep's residual).
+//
+// A wave owns 64 float4 column chunks; lanes 0 and 63 are halo lanes whose
+// values go stale one element per sweep from the outside in, so for T <= 4
+// lanes 1..62 (248 columns) stay exact and are the only ones stored; wave
+// columns overlap by two chunks.  The wave marches a segment of R output rows
+// through T pipelined stages: at row slot k it loads input row k and stage s
+// (1..T) computes row k-s from stage s-1's window of rows k-s-1..k-s+1, so
+// every stage is one sweep of the reference, at R + 2T row slots per segment.
+// p' and rhs come from HBM once per launch (12 B per T cell-updates).
+//
+// Per stage the p' boundary conditions of model.rs:807-815 are applied to the
+// window itself: column 0 takes column 1, column nx-1 is 0, global row ny-1
+// copies row ny-2, and global row 0 is patched with row 1 as soon as row 1 is
+// computed (before the next stage reads it).  Only the final stage is stored,
+// with the same fused boundary stores as k_jacobi.
+template <int T, int R, int FAST>
+__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, int pass, int it, int out_lo, int out_hi, int nwc) {
+    if (pass_off(ctl, pass)) return;
+    const int nx = g.nx, nch = nx >> 2, hg = g.hg, nyl = g.nyl;
+    const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    const int wc = (int)blockIdx.x % nwc;
+    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
+    const int r0 = out_lo + seg * R;
+    const int r1 = min(r0 + R, out_hi);
+    if (r0 >= r1) return;                                  // wave-uniform
+    const int ch = wc * 62 - 1 + lane;
+    const bool in_dom = ch >= 0 && ch < nch;
+    const bool out_lane = in_dom && lane >= 1 && lane <= 62;
+
+    const int si = (ctl->cur + it) & 1;
+    float *src_alloc = si ? pb : pa;
+    float *dst_alloc = si ? pa : pb;
+    const int pbytes = (nyl + 2 * hg) * nx * 4;
+    const __amdgpu_buffer_rsrc_t rs_p =
+        __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_r =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)hg * nx), 0, pbytes, 0x00020000);
+    float *__restrict__ dst = dst_alloc + (long)hg * nx;
+
+    const float dx_sq = g.dx_sq, dy_sq = g.dy_sq, denom = g.denom;
+    const float r_dx_sq = g.r_dx_sq, r_dy_sq = g.r_dy_sq, r_denom = g.r_denom;
+    const float omega = 0.75f;
+    const float om1 = 1.0f - omega;
+    constexpr int kOOB = -16;
+    const int col = 4 * ch;
+    const int row_bytes = nx * 4;
+    const int off0 = in_dom ? (hg * nx + col) * 4 : kOOB;
+    auto ld4 = [&](const __amdgpu_buffer_rsrc_t &rs, int row) -> float4 {
+        const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                           __uint_as_float(v.w));
+    };
+    const bool e0 = (col >= 1) && (col <= nx - 8);
+    const bool e1 = (col + 1 <= nx - 8);
+    const bool e2 = (col + 2 <= nx - 8);
+    const bool e3 = (col + 3 <= nx - 8);
+    const int g_first = 1 - g.j0, g_last = g.ny - 2 - g.j0, g_top = g.ny - 1 - g.j0;
+    const int g_zero = -g.j0;
+
+    // one sweep of one row from the window (B, C, Tp) of the previous stage
+    auto stage = [&](const float4 &B, const float4 &Cc, const float4 &Tp,
+                     const float4 &Rh) -> float4 {
+        const float L0 = __shfl_up(Cc.w, 1, 64);
+        const float R3 = __shfl_down(Cc.x, 1, 64);
+        const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
+        const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
+        const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
+        const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
+        const float bb[4] = {B.x, B.y, B.z, B.w};
+        const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
+        float n[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
+            const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
+            const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
+            n[k] = omega * p_update + om1 * cc[k];
+        }
+        float4 o = make_float4(n[0], n[1], n[2], n[3]);
+        if (ch == 0) o.x = n[1];
+        if (ch == nch - 1) o.w = 0.0f;
+        return o;
+    };
+
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 W[T][3];      // W[s] = stage-s rows (k-s-2, k-s-1, k-s); stage 0 = input
+    float4 RH[T];        // RH[s] = rhs row k-1-s
+#pragma unroll
+    for (int s = 0; s < T; ++s) {
+        W[s][0] = W[s][1] = W[s][2] = z4;
+        RH[s] = z4;
+    }
+    const int k_first = r0 - T, k_last = r1 + T - 1;
+    float4 pfP0 = ld4(rs_p, k_first), pfR0 = ld4(rs_r, k_first - 1);
+    float4 pfP1 = ld4(rs_p, k_first + 1), pfR1 = ld4(rs_r, k_first);
+    float m = 0.0f;
+    for (int k = k_first; k <= k_last; ++k) {
+        const float4 inP = pfP0, inR = pfR0;
+        pfP0 = pfP1;
+        pfR0 = pfR1;
+        pfP1 = ld4(rs_p, k + 2);
+        pfR1 = ld4(rs_r, k + 1);
+        W[0][0] = W[0][1];
+        W[0][1] = W[0][2];
+        W[0][2] = inP;
+#pragma unroll
+        for (int s = T - 1; s >= 1; --s) RH[s] = RH[s - 1];
+        RH[0] = inR;
+#pragma unroll
+        for (int s = 1; s <= T; ++s) {
+            const int r = k - s;
+            if (k < r0 - T + 2 * s) continue;              // row not needed yet
+            float4 n = stage(W[s - 1][0], W[s - 1][1], W[s - 1][2], RH[s - 1]);
+            if (s < T) {
+                if (r == g_top) n = W[s][2];               // P(i,ny-1) = P(i,ny-2)
+                W[s][0] = W[s][1];
+                W[s][1] = W[s][2];
+                W[s][2] = n;
+                if (r == g_first) W[s][1] = n;             // P(i,0) = P(i,1)
+            } else if (r >= r0 && r < r1) {
+                if (r >= 0 && r < nyl) {
+                    const float4 C = W[T - 1][1];
+                    if (out_lane) {
+                        if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                        if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                        if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                        if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                    }
+                }
+                if (out_lane) {
+                    *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
+                    if (r == g_first)
+                        *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
+                    if (r == g_last)
+                        *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
+                }
+            }
+        }
+    }
+    m = wave_max(m);
+    if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
 // End of a pressure solve: how many sweeps ran, which buffer is current, the
@@ -640,9 +828,51 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
     const int nwc = cdiv(nch, 64);
     const int nbx = cdiv(nwc, kJacWavesPerBlock);
     const int nseg = cdiv(row_hi - row_lo, kJacRowsPerWave);
-    hipLaunchKernelGGL(k_jacobi<kJacRowsPerWave>, dim3(nbx * nseg),
-                       dim3(kJacWavesPerBlock * 64), 0, s, g, f.pp[0] - (long)g.hg * g.nx,
-                       f.pp[1] - (long)g.hg * g.nx, f.rhs, f.ctl, pass, it, row_lo, row_hi, nbx);
+    float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
+    const dim3 grid(nbx * nseg), block(kJacWavesPerBlock * 64);
+    if (g.fastdiv == 1)
+        hipLaunchKernelGGL((k_jacobi<kJacRowsPerWave, 1>), grid, block, 0, s, g, pa, pb, f.rhs,
+                           f.ctl, pass, it, row_lo, row_hi, nbx);
+    else if (g.fastdiv == 2)
+        hipLaunchKernelGGL((k_jacobi<kJacRowsPerWave, 2>), grid, block, 0, s, g, pa, pb, f.rhs,
+                           f.ctl, pass, it, row_lo, row_hi, nbx);
+    else
+        hipLaunchKernelGGL((k_jacobi<kJacRowsPerWave, 0>), grid, block, 0, s, g, pa, pb, f.rhs,
+                           f.ctl, pass, it, row_lo, row_hi, nbx);
+}
+
+template <int T>
+static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int out_lo, int out_hi,
+                      hipStream_t s) {
+    const int nch = g.nx / 4;
+    const int nwc = cdiv(nch, 62);
+    const int nseg = cdiv(out_hi - out_lo, kTbRowsPerWave);
+    const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
+    float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
+    if (g.fastdiv == 1)
+        hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 1>), grid, block, 0, s, g, pa, pb,
+                           f.rhs, f.ctl, pass, it, out_lo, out_hi, nwc);
+    else if (g.fastdiv == 2)
+        hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 2>), grid, block, 0, s, g, pa, pb,
+                           f.rhs, f.ctl, pass, it, out_lo, out_hi, nwc);
+    else
+        hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 0>), grid, block, 0, s, g, pa, pb,
+                           f.rhs, f.ctl, pass, it, out_lo, out_hi, nwc);
+}
+
+void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int T, int out_lo,
+                         int out_hi, hipStream_t s) {
+    if (out_hi <= out_lo) return;
+    switch (T) {
+    case 1: launch_tb<1>(g, f, pass, it, out_lo, out_hi, s); break;
+    case 2: launch_tb<2>(g, f, pass, it, out_lo, out_hi, s); break;
+    case 3: launch_tb<3>(g, f, pass, it, out_lo, out_hi, s); break;
+    default: launch_tb<4>(g, f, pass, it, out_lo, out_hi, s); break;
+    }
+}
+
+void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s) {
+    hipLaunchKernelGGL(k_verify_division, dim3(8192), dim3(kBlock), 0, s, c, r, dev_counts);
 }
 
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,

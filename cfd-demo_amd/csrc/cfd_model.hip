@@ -105,6 +105,7 @@ struct cfd_model {
     ncclComm_t comm = nullptr;
     LocalHub *hub = nullptr;   // testing stand-in for comm
     int host_cur = 0;   // mirror of ctl->cur, valid when the tolerance is off
+    int t_max = kMaxTemporal;   // sweeps per temporally blocked launch (CFD_TEMPORAL)
     // timing
     hipEvent_t ev_step0 = nullptr, ev_step1 = nullptr, ev_prof0 = nullptr, ev_prof1 = nullptr;
     bool timing = false;
@@ -236,10 +237,35 @@ struct cfd_model {
             e1 = take_event();
             HIP_TRY(hipEventRecord(e0, stream));
         }
+        const int tmax = g.tol_enabled ? 1 : t_max;
         if (!sharded()) {
-            for (int it = 0; it < iters; ++it)
-                launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
+            if (tmax <= 1) {
+                for (int it = 0; it < iters; ++it)
+                    launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
+            } else {
+                for (int it = 0; it < iters;) {
+                    int T, lo, hi, exch;
+                    plan_block((int)j0, g.nyl, g.ny, 0, it, tmax, iters, &T, &lo, &hi, &exch);
+                    launch_jacobi_block(g, f, pass, it, T, lo, hi, stream);
+                    it += T;
+                }
+            }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
+        } else if (tmax > 1) {
+            int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
+            if (rc0) return rc0;
+            for (int it = 0; it < iters;) {
+                int T, lo, hi, exch;
+                plan_block(g.j0, g.nyl, g.ny, g.hg, it, tmax, iters, &T, &lo, &hi, &exch);
+                launch_jacobi_block(g, f, pass, it, T, lo, hi, stream);
+                it += T;
+                if (exch) {
+                    int rc = exchange_pp((host_cur + it) & 1, g.hg);
+                    if (rc) return rc;
+                }
+            }
+            int rc = allreduce_max_u32(f.ctl->err + (iters > 0 ? iters - 1 : 0), 1);
+            if (rc) return rc;
         } else {
             // the deep-halo sweeps recompute ghost rows, which read rhs there
             int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
@@ -432,6 +458,55 @@ void apply_params(cfd_model *m, const cfd_params *p) {
     m->g.jacobi_iters = p->jacobi_iters;
 }
 
+// Pick the cheapest division form that is bit-identical to IEEE `/` for ALL
+// 2^32 f32 inputs, for each of the three Jacobi divisors, by exhaustive
+// check on the device (a few ms; cached per divisor value).  x * RN(1/c) is
+// exact e.g. for the power-of-two divisors of the 2^k cavity grids; the
+// FMA-corrected form covers most other divisors; anything else keeps IEEE
+// division.  CFD_FASTDIV=0 forces IEEE.
+std::mutex g_div_mu;
+std::vector<std::pair<uint32_t, int>> g_div_cache;   // divisor bits -> ok mask (bit0 m1, bit1 m2)
+
+int division_ok_mask(hipStream_t s, float c, float r, int *mask) {
+    uint32_t bits;
+    std::memcpy(&bits, &c, 4);
+    {
+        std::lock_guard<std::mutex> lk(g_div_mu);
+        for (auto &e : g_div_cache)
+            if (e.first == bits) {
+                *mask = e.second;
+                return 0;
+            }
+    }
+    unsigned long long *d = nullptr, h[2] = {0, 0};
+    HIP_TRY(hipMalloc((void **)&d, 16));
+    HIP_TRY(hipMemsetAsync(d, 0, 16, s));
+    launch_verify_division(c, r, d, s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipFree(d));
+    *mask = (h[0] == 0 ? 1 : 0) | (h[1] == 0 ? 2 : 0);
+    std::lock_guard<std::mutex> lk(g_div_mu);
+    g_div_cache.emplace_back(bits, *mask);
+    return 0;
+}
+
+int choose_division(hipStream_t s, Geom &g) {
+    g.fastdiv = 0;
+    const char *env = getenv("CFD_FASTDIV");
+    if (env && atoi(env) == 0) return 0;
+    int m1, m2, m3;
+    int rc;
+    if ((rc = division_ok_mask(s, g.dx_sq, g.r_dx_sq, &m1)) ||
+        (rc = division_ok_mask(s, g.dy_sq, g.r_dy_sq, &m2)) ||
+        (rc = division_ok_mask(s, g.denom, g.r_denom, &m3)))
+        return rc;
+    const int all = m1 & m2 & m3;
+    g.fastdiv = (all & 1) ? 1 : (all & 2) ? 2 : 0;
+    return 0;
+}
+
 // Model::new (model.rs:219-299), restricted to rows [j0, j1) of the slab.
 int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int device, int hg) {
     m->device = device;
@@ -453,6 +528,18 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     g.dy = grid->ly / (float)grid->ny;   // src/app.rs:38
     g.ly = grid->ly;
     apply_params(m, p);
+    // Jacobi divisors exactly as jacobi_pressure forms them (model.rs:740-746)
+    g.dx_sq = g.dx * g.dx;
+    g.dy_sq = g.dy * g.dy;
+    g.denom = 2.0f / (g.dx * g.dx) + 2.0f / (g.dy * g.dy);
+    g.r_dx_sq = 1.0f / g.dx_sq;
+    g.r_dy_sq = 1.0f / g.dy_sq;
+    g.r_denom = 1.0f / g.denom;
+    {
+        int rc0 = choose_division(m->stream, g);
+        if (rc0) return rc0;
+    }
+    if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, std::min(kMaxTemporal, atoi(tv)));
 
     const size_t W = (size_t)nx + 1, nyl = (size_t)g.nyl;
     const size_t u_alloc = round4(m->u_rows_alloc() * W);
@@ -916,6 +1003,13 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
 }
 
 int cfd_get_halo_depth(const cfd_model *m) { return m ? m->g.hg : 0; }
+
+int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (fastdiv) *fastdiv = m->g.fastdiv;
+    if (temporal) *temporal = m->g.tol_enabled ? 1 : m->t_max;
+    return 0;
+}
 
 // ---- host-only slab plan (no device needed) ----
 int cfd_plan_slab(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1) {

@@ -35,6 +35,28 @@ inline void plan_sweep(int j0, int nyl, int ny, int hg, int it, int iters, int *
     *exchange = (s == hg - 1 || it == iters - 1) ? 1 : 0;
 }
 
+// Temporally blocked form: the block of sweeps starting at `it` runs
+// *T = min(t_max, sweeps left before the next exchange, sweeps left in the
+// solve) sweeps in one launch and stores its final sweep on local rows
+// [out_lo, out_hi) (= what plan_sweep gives for the block's last sweep);
+// *exchange as in plan_sweep.  hg <= 0 means unsharded (no exchanges).
+inline void plan_block(int j0, int nyl, int ny, int hg, int it, int t_max, int iters, int *T,
+                       int *out_lo, int *out_hi, int *exchange) {
+    const int lo_g = 1 - j0, hi_g = ny - 1 - j0;
+    if (hg <= 0) {
+        *T = std::min(t_max, iters - it);
+        *out_lo = lo_g;
+        *out_hi = hi_g;
+        *exchange = 0;
+        return;
+    }
+    const int s = it % hg;
+    *T = std::min(std::min(t_max, hg - s), iters - it);
+    int ex;
+    plan_sweep(j0, nyl, ny, hg, it + *T - 1, iters, out_lo, out_hi, &ex);
+    *exchange = ex;
+}
+
 // Halo geometry for one field, in local rows:
 //   out[0..2] = {send_start, recv_start, rows} with the rank below (rank-1)
 //   out[3..5] = {send_start, recv_start, rows} with the rank above (rank+1)

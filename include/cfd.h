@@ -179,6 +179,10 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
                    uint64_t *steps);
 /* p' halo depth (rows exchanged per RCCL round) of a sharded model. */
 int cfd_get_halo_depth(const cfd_model *m);
+/* Jacobi kernel configuration chosen at creation: division form proven exact
+ * for this grid's divisors (0 IEEE, 1 reciprocal multiply, 2 FMA-corrected)
+ * and sweeps per launch (1 when the tolerance is on). */
+int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal);
 
 /* Host-only slab plan used by cfd_create_sharded (no device needed; the
  * multi-rank CPU tests drive the same plan):

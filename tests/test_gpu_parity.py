@@ -237,3 +237,42 @@ def test_control_handle_run_loop():
     assert snap is not None and snap.paused and snap.u.size == 65 * 32
     h.stop()
     h.join(10)
+
+
+@pytest.mark.parametrize("fastdiv,temporal", [("0", "1"), ("0", "4"), ("1", "1"), ("1", "3"),
+                                              ("1", "4")])
+def test_kernel_variants_bitwise(monkeypatch, fastdiv, temporal):
+    """Every Jacobi kernel variant (IEEE or proven-exact fast division; 1..4
+    sweeps per launch) gives the oracle's bits, on a power-of-two cavity (where
+    the reciprocal multiply is exact) and on the reference's default channel
+    grid (non-power-of-two divisors)."""
+    c = _cfd()
+    monkeypatch.setenv("CFD_FASTDIV", fastdiv)
+    monkeypatch.setenv("CFD_TEMPORAL", temporal)
+    cases = [
+        (dict(nx=256, ny=128, lx=2.0, ly=1.0, cylinder=None),
+         dict(bc_kind=1, viscosity=0.001, jacobi_iters=23, corrector_passes=1, tol_enabled=0)),
+        (dict(nx=800, ny=264, lx=30.0, ly=10.0, cylinder=(7.5, 5.0, 0.75)),
+         dict(jacobi_iters=30, corrector_passes=2, tol_enabled=0)),
+    ]
+    for g, kw in cases:
+        o = _oracle(g, **kw)
+        m = c.Model(_grid(g), _params(kw))
+        cfg = m.kernel_config
+        assert cfg["temporal"] == int(temporal)
+        if fastdiv == "0":
+            assert cfg["fastdiv"] == 0
+        for _ in range(4):
+            o.update()
+            m.update()
+        st = m.get_state()
+        for f in ("u", "v", "p", "p_prime"):
+            assert_bitwise(f"{g['nx']}x{g['ny']} fd={cfg['fastdiv']} T={temporal}:{f}", st[f],
+                           o.field(f))
+
+
+def test_power_of_two_cavity_uses_reciprocal_multiply():
+    c = _cfd()
+    m = c.Model(c.cavity_grid(4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
+                                                               tol_enabled=False))
+    assert m.kernel_config == {"fastdiv": 1, "temporal": 4}
