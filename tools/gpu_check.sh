@@ -22,4 +22,9 @@ if [ "${PROFILE:-1}" = 1 ]; then
   export TMPDIR=/tmp
   step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline
 fi
+if [ "${PMC:-0}" = 1 ]; then
+  export TMPDIR=/tmp
+  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_$TAG -o fetch --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_$TAG -o write --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+fi
 echo DONE
