@@ -145,7 +145,7 @@ def main():
     cells_local = nx * model.nyl
     kcfg = model.kernel_config
     T = kcfg["temporal"]
-    launches = max(tm["sweeps"] // T, 1)
+    launches = max(args.steps * -(-args.iters // T), 1)   # ceil(iters / T) launches per solve
     launch_ms = tm["solve_ms"] / launches
     # algorithmic bytes per launch = 12 B/cell-update x cells x sweeps per launch
     bytes_launch = BYTES_PER_CELL_UPDATE * cells_local * T

@@ -18,7 +18,7 @@ EXPORTS = [
     "cfd_pressure_solve", "cfd_run_phase", "cfd_set_params", "cfd_get_snapshot",
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
-    "cfd_get_kernel_config", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo",
+    "cfd_get_kernel_config", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block",
     "cfd_last_error", "cfd_abi_version", "cfd_destroy",
 ]
 
@@ -110,6 +110,8 @@ def load():
         "cfd_plan_sweep": (i32, [i32, i32, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i32),
                                  C.POINTER(i32)]),
         "cfd_plan_halo": (i32, [i32, i32, i32, i32, i32, C.POINTER(i32)]),
+        "cfd_plan_block": (i32, [i32, i32, i32, i32, i32, i32, i32, C.POINTER(i32),
+                                 C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "cfd_last_error": (C.c_char_p, []),
         "cfd_abi_version": (i32, []),
         "cfd_destroy": (None, [vp]),

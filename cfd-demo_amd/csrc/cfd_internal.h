@@ -89,13 +89,17 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
 // T consecutive Jacobi sweeps in one launch (temporal blocking, tolerance
 // off): the final sweep's rows [out_lo, out_hi) are stored; sweep `it` of the
 // block is the first.  T <= kMaxTemporal.
-void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int T, int out_lo,
-                         int out_hi, hipStream_t s);
+// `par` = launches of this solve before this one (selects the source buffer:
+// buffers flip once per launch).
+void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
+                         int out_lo, int out_hi, hipStream_t s);
 // Exhaustive check over all 2^32 f32 inputs x of x/c against the two fast
 // forms; writes mismatch counts {mode1, mode2} to dev_counts (2 x u64).
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s);
+// flips = launches of a fixed-count solve (ignored with the tolerance on,
+// where each executed sweep is one launch).
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
-                           hipStream_t s);
+                           int flips, hipStream_t s);
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s);
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);

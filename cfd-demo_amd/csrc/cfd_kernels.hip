@@ -459,7 +459,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
 template <int T, int R, int FAST>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int out_lo, int out_hi, int nwc) {
+    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc) {
     if (pass_off(ctl, pass)) return;
     const int nx = g.nx, nch = nx >> 2, hg = g.hg, nyl = g.nyl;
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
@@ -472,7 +472,8 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     const bool in_dom = ch >= 0 && ch < nch;
     const bool out_lane = in_dom && lane >= 1 && lane <= 62;
 
-    const int si = (ctl->cur + it) & 1;
+    // buffers ping-pong once per LAUNCH: par = launches since the solve began
+    const int si = (ctl->cur + par) & 1;
     float *src_alloc = si ? pb : pa;
     float *dst_alloc = si ? pa : pb;
     const int pbytes = (nyl + 2 * hg) * nx * 4;
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
 // returned residual (model.rs:816-823), and whether the corrector loop goes on
 // (model.rs:721-723).  Resets the per-sweep slots for the next solve.
 __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
-                                                           int check_break) {
+                                                           int check_break, int flips) {
     Ctl *c = f.ctl;
     __shared__ int go_s;
     if (threadIdx.x == 0) {
@@ -603,7 +604,9 @@ __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int
                 while (n < iters && __uint_as_float(c->err[n - 1]) >= g.p_tol) ++n;
             }
             const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
-            c->cur = (c->cur + n) & 1;
+            // one buffer flip per launch: per sweep with the tolerance on,
+            // `flips` (host-known launch count) for fixed-count solves
+            c->cur = (c->cur + (g.tol_enabled ? n : flips)) & 1;
             c->last_p = res;
             c->n_exec_last = (uint32_t)n;
             c->sweeps_total += (uint64_t)n;
@@ -842,8 +845,8 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
 }
 
 template <int T>
-static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int out_lo, int out_hi,
-                      hipStream_t s) {
+static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par, int out_lo,
+                      int out_hi, hipStream_t s) {
     const int nch = g.nx / 4;
     const int nwc = cdiv(nch, 62);
     const int nseg = cdiv(out_hi - out_lo, kTbRowsPerWave);
@@ -851,23 +854,23 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int out_
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 1>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, out_lo, out_hi, nwc);
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc);
     else if (g.fastdiv == 2)
         hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 2>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, out_lo, out_hi, nwc);
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc);
     else
         hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 0>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, out_lo, out_hi, nwc);
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc);
 }
 
-void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int T, int out_lo,
-                         int out_hi, hipStream_t s) {
+void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
+                         int out_lo, int out_hi, hipStream_t s) {
     if (out_hi <= out_lo) return;
     switch (T) {
-    case 1: launch_tb<1>(g, f, pass, it, out_lo, out_hi, s); break;
-    case 2: launch_tb<2>(g, f, pass, it, out_lo, out_hi, s); break;
-    case 3: launch_tb<3>(g, f, pass, it, out_lo, out_hi, s); break;
-    default: launch_tb<4>(g, f, pass, it, out_lo, out_hi, s); break;
+    case 1: launch_tb<1>(g, f, pass, it, par, out_lo, out_hi, s); break;
+    case 2: launch_tb<2>(g, f, pass, it, par, out_lo, out_hi, s); break;
+    case 3: launch_tb<3>(g, f, pass, it, par, out_lo, out_hi, s); break;
+    default: launch_tb<4>(g, f, pass, it, par, out_lo, out_hi, s); break;
     }
 }
 
@@ -876,9 +879,9 @@ void launch_verify_division(float c, float r, unsigned long long *dev_counts, hi
 }
 
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
-                           hipStream_t s) {
+                           int flips, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize_solve, dim3(1), dim3(kBlock), 0, s, g, f, pass, iters,
-                       check_break);
+                       check_break, flips);
 }
 
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,

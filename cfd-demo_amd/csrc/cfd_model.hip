@@ -112,7 +112,7 @@ struct cfd_model {
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> solve_events;
     size_t ev_next = 0;
-    uint64_t timed_sweeps = 0, timed_steps = 0;
+    uint64_t timed_sweeps = 0, timed_steps = 0, timed_launches = 0;
     double timed_step_ms = 0.0;
     bool stepped = false;
 
@@ -238,58 +238,52 @@ struct cfd_model {
             HIP_TRY(hipEventRecord(e0, stream));
         }
         const int tmax = g.tol_enabled ? 1 : t_max;
+        int launches = 0;   // buffers flip once per launch
         if (!sharded()) {
             if (tmax <= 1) {
                 for (int it = 0; it < iters; ++it)
                     launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
+                launches = iters;
             } else {
                 for (int it = 0; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, tmax, iters, &T, &lo, &hi, &exch);
-                    launch_jacobi_block(g, f, pass, it, T, lo, hi, stream);
+                    launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, stream);
                     it += T;
+                    ++launches;
                 }
             }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
-        } else if (tmax > 1) {
+        } else {
+            // the deep-halo sweeps recompute ghost rows, which read rhs there
             int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
             if (rc0) return rc0;
             for (int it = 0; it < iters;) {
                 int T, lo, hi, exch;
                 plan_block(g.j0, g.nyl, g.ny, g.hg, it, tmax, iters, &T, &lo, &hi, &exch);
-                launch_jacobi_block(g, f, pass, it, T, lo, hi, stream);
+                if (tmax == 1)
+                    launch_jacobi_sweep(g, f, pass, it, lo, hi, stream);
+                else
+                    launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, stream);
                 it += T;
+                ++launches;
                 if (exch) {
-                    int rc = exchange_pp((host_cur + it) & 1, g.hg);
+                    int rc = exchange_pp((host_cur + launches) & 1, g.hg);
                     if (rc) return rc;
                 }
             }
             int rc = allreduce_max_u32(f.ctl->err + (iters > 0 ? iters - 1 : 0), 1);
             if (rc) return rc;
-        } else {
-            // the deep-halo sweeps recompute ghost rows, which read rhs there
-            int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
-            if (rc0) return rc0;
-            for (int it = 0; it < iters; ++it) {
-                int lo, hi, exch;
-                plan_sweep(g.j0, g.nyl, g.ny, g.hg, it, iters, &lo, &hi, &exch);
-                launch_jacobi_sweep(g, f, pass, it, lo, hi, stream);
-                if (exch) {
-                    int rc = exchange_pp((host_cur + it + 1) & 1, g.hg);
-                    if (rc) return rc;
-                }
-            }
-            int rc = allreduce_max_u32(f.ctl->err + (iters > 0 ? iters - 1 : 0), 1);
-            if (rc) return rc;
+            if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
         }
-        if (evt && sharded()) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
-        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, stream);
+        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream);
         HIP_TRY(hipGetLastError());
         if (evt) {
             solve_events.emplace_back(e0, e1);
             timed_sweeps += (uint64_t)iters;
+            timed_launches += (uint64_t)launches;
         }
-        host_cur = (host_cur + iters) & 1;
+        host_cur = (host_cur + launches) & 1;
         return 0;
     }
 
@@ -314,7 +308,7 @@ struct cfd_model {
             if (params.tol_enabled && e < params.p_tol) break;
         }
         // the device finalize recomputes n from the (identical) all-reduced slots
-        launch_finalize_solve(g, f, -1, iters, 0, stream);
+        launch_finalize_solve(g, f, -1, iters, 0, n, stream);
         HIP_TRY(hipGetLastError());
         host_cur = (host_cur + n) & 1;
         float res = 0.f;
@@ -950,7 +944,7 @@ int cfd_profile_sweeps(cfd_model *m, int n_sweeps, double *avg_ms_out) {
     HIP_TRY(hipEventRecord(a, m->stream));
     for (int it = 0; it < n_sweeps; ++it) launch_jacobi_sweep(g, m->f, -1, it, lo, hi, m->stream);
     HIP_TRY(hipEventRecord(b, m->stream));
-    launch_finalize_solve(g, m->f, -1, n_sweeps, 0, m->stream);
+    launch_finalize_solve(g, m->f, -1, n_sweeps, 0, n_sweeps, m->stream);
     HIP_TRY(hipGetLastError());
     m->host_cur = (m->host_cur + n_sweeps) & 1;
     int rc = m->sync();
@@ -972,6 +966,7 @@ int cfd_timing_begin(cfd_model *m) {
     m->solve_events.clear();
     m->step_events.clear();
     m->timed_sweeps = 0;
+    m->timed_launches = 0;
     m->timed_steps = 0;
     return 0;
 }
@@ -1023,6 +1018,14 @@ int cfd_plan_sweep(int j0, int nyl, int ny, int halo_depth, int it, int iters, i
                    int *exchange) {
     if (halo_depth < 1 || !lo || !hi || !exchange) return fail(CFD_EINVAL, "bad plan_sweep arguments");
     plan_sweep(j0, nyl, ny, halo_depth, it, iters, lo, hi, exchange);
+    return 0;
+}
+
+int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, int iters, int *T,
+                   int *out_lo, int *out_hi, int *exchange) {
+    if (t_max < 1 || !T || !out_lo || !out_hi || !exchange)
+        return fail(CFD_EINVAL, "bad plan_block arguments");
+    plan_block(j0, nyl, ny, halo_depth, it, t_max, iters, T, out_lo, out_hi, exchange);
     return 0;
 }
 

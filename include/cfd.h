@@ -197,6 +197,11 @@ int cfd_plan_slab(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1
 int cfd_plan_sweep(int j0, int nyl, int ny, int halo_depth, int it, int iters, int *lo, int *hi,
                    int *exchange);
 int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6);
+/* Temporally blocked form of cfd_plan_sweep: the launch starting at sweep
+ * `it` runs *T <= t_max sweeps and stores its last sweep on local rows
+ * [out_lo, out_hi); halo_depth <= 0 means unsharded. */
+int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, int iters, int *T,
+                   int *out_lo, int *out_hi, int *exchange);
 
 const char *cfd_last_error(void);
 int cfd_abi_version(void);

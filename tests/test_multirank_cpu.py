@@ -46,6 +46,13 @@ def plan_sweep(j0, nyl, ny, hg, it, iters):
     return lo.value, hi.value, bool(ex.value)
 
 
+def plan_block(j0, nyl, ny, hg, it, t_max, iters):
+    T, lo, hi, ex = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    assert _lib().cfd_plan_block(j0, nyl, ny, hg, it, t_max, iters, C.byref(T), C.byref(lo),
+                                 C.byref(hi), C.byref(ex)) == 0
+    return T.value, lo.value, hi.value, bool(ex.value)
+
+
 def plan_halo(kind, nyl, depth, r, n):
     out = (C.c_int * 6)()
     assert _lib().cfd_plan_halo(kind, nyl, depth, r, n, out) == 0
@@ -99,7 +106,7 @@ def _worker(rank, n, port, cases, results):
     dist.init_process_group("gloo", rank=rank, world_size=n)
     try:
         out = []
-        for (nx, ny, hg, iters, seed) in cases:
+        for (nx, ny, hg, iters, seed, t_max) in cases:
             rng = np.random.default_rng(seed)
             P = rng.uniform(-1, 1, (ny, nx)).astype(F)
             RHS = rng.uniform(-1, 1, (ny, nx)).astype(F)
@@ -116,10 +123,23 @@ def _worker(rank, n, port, cases, results):
             exchange(bufs[0], g0, plan_halo(2, nyl, hg, rank, n), rank, n)
             exchange(rhs, g0, plan_halo(2, nyl, hg, rank, n), rank, n)
             cur = 0
-            for it in range(iters):
-                lo, hi, ex = plan_sweep(j0, nyl, ny, hg, it, iters)
-                sweep_rows(bufs[cur], bufs[cur ^ 1], rhs, g0, lo, hi, nx, ny, j0, dx, dy)
-                cur ^= 1
+            it = 0
+            while it < iters:
+                if t_max == 1:
+                    lo, hi, ex = plan_sweep(j0, nyl, ny, hg, it, iters)
+                    sweep_rows(bufs[cur], bufs[cur ^ 1], rhs, g0, lo, hi, nx, ny, j0, dx, dy)
+                    cur ^= 1
+                    it += 1
+                else:
+                    # k_jacobi_tb: T sweeps, sweep s recomputing T-1-s extra rows
+                    # each side of the stored band (clipped to global 1..ny-2)
+                    T, lo, hi, ex = plan_block(j0, nyl, ny, hg, it, t_max, iters)
+                    for s_ in range(T):
+                        e = T - 1 - s_
+                        a, b = max(lo - e, 1 - j0), min(hi + e, ny - 1 - j0)
+                        sweep_rows(bufs[cur], bufs[cur ^ 1], rhs, g0, a, b, nx, ny, j0, dx, dy)
+                        cur ^= 1
+                    it += T
                 if ex:
                     exchange(bufs[cur], g0, plan_halo(2, nyl, hg, rank, n), rank, n)
             mine = torch.from_numpy(np.ascontiguousarray(bufs[cur][g0:g0 + nyl]))
@@ -159,12 +179,16 @@ def _free_port():
     return p
 
 
-CASES = [  # nx, ny, halo depth, sweeps, seed
-    (16, 40, 1, 5, 1),
-    (24, 40, 3, 7, 2),
-    (32, 44, 8, 20, 3),
-    (16, 30, 4, 4, 4),
-    (16, 37, 2, 9, 5),
+CASES = [  # nx, ny, halo depth, sweeps, seed, sweeps per launch
+    (16, 40, 1, 5, 1, 1),
+    (24, 40, 3, 7, 2, 1),
+    (32, 44, 8, 20, 3, 1),
+    (16, 30, 4, 4, 4, 1),
+    (16, 37, 2, 9, 5, 1),
+    (16, 40, 8, 21, 6, 4),
+    (24, 44, 6, 13, 7, 4),
+    (16, 37, 3, 10, 8, 2),
+    (16, 40, 5, 12, 9, 3),
 ]
 
 
@@ -183,7 +207,7 @@ def test_sharded_jacobi_plan_matches_single_domain(n):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for (nx, ny, hg, iters, seed), res in zip(CASES, got):
+    for (nx, ny, hg, iters, seed, _), res in zip(CASES, got):
         rng = np.random.default_rng(seed)
         P = rng.uniform(-1, 1, (ny, nx)).astype(F)
         RHS = rng.uniform(-1, 1, (ny, nx)).astype(F)
