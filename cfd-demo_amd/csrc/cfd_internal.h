@@ -61,6 +61,7 @@ struct Geom {
     float dx_sq, dy_sq, denom;
     float r_dx_sq, r_dy_sq, r_denom;
     int32_t fastdiv;
+    int32_t tb_rows;      // output rows per wave segment of k_jacobi_tb (0: default)
 };
 
 struct Fields {

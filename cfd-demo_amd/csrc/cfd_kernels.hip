@@ -456,57 +456,38 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
 // copies row ny-2, and global row 0 is patched with row 1 as soon as row 1 is
 // computed (before the next stage reads it).  Only the final stage is stored,
 // with the same fused boundary stores as k_jacobi.
-template <int T, int R, int FAST>
-__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
-    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc) {
-    if (pass_off(ctl, pass)) return;
-    const int nx = g.nx, nch = nx >> 2, hg = g.hg, nyl = g.nyl;
-    const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    const int wc = (int)blockIdx.x % nwc;
-    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
-    const int r0 = out_lo + seg * R;
-    const int r1 = min(r0 + R, out_hi);
-    if (r0 >= r1) return;                                  // wave-uniform
-    const int ch = wc * 62 - 1 + lane;
-    const bool in_dom = ch >= 0 && ch < nch;
-    const bool out_lane = in_dom && lane >= 1 && lane <= 62;
+// Per-wave state of k_jacobi_tb.  Register rings are indexed by the slot
+// number v (0-based within the segment) modulo their period, so with the slot
+// loop unrolled by 6 (= lcm of the periods 2, 3 and 6) every index is a
+// compile-time constant and no window ever moves between registers:
+//   PF[v % 2]        p' input row k_first+v, loaded two slots ahead
+//   W[s][v % 3]      newest row of stage s (stage 0 = input)
+//   RH[(q-k_first+1) % 6]  rhs row q (rows k-4 .. k+1 live at slot k)
+template <int T, int FAST>
+struct TbWave {
+    float4 W[T][3];
+    float4 RH[6];
+    float4 PF[2];
+    // geometry (wave-uniform scalars unless noted)
+    int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
+    int ch, col, lane, off0;    // per lane
+    bool out_lane, e0, e1, e2, e3;
+    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
+    __amdgpu_buffer_rsrc_t rs_p, rs_r;
+    float *dst;
+    float m;
 
-    // buffers ping-pong once per LAUNCH: par = launches since the solve began
-    const int si = (ctl->cur + par) & 1;
-    float *src_alloc = si ? pb : pa;
-    float *dst_alloc = si ? pa : pb;
-    const int pbytes = (nyl + 2 * hg) * nx * 4;
-    const __amdgpu_buffer_rsrc_t rs_p =
-        __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_r =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)hg * nx), 0, pbytes, 0x00020000);
-    float *__restrict__ dst = dst_alloc + (long)hg * nx;
-
-    const float dx_sq = g.dx_sq, dy_sq = g.dy_sq, denom = g.denom;
-    const float r_dx_sq = g.r_dx_sq, r_dy_sq = g.r_dy_sq, r_denom = g.r_denom;
-    const float omega = 0.75f;
-    const float om1 = 1.0f - omega;
-    constexpr int kOOB = -16;
-    const int col = 4 * ch;
-    const int row_bytes = nx * 4;
-    const int off0 = in_dom ? (hg * nx + col) * 4 : kOOB;
-    auto ld4 = [&](const __amdgpu_buffer_rsrc_t &rs, int row) -> float4 {
+    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int row) const {
+        constexpr int kOOB = -16;
         const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
         return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                            __uint_as_float(v.w));
-    };
-    const bool e0 = (col >= 1) && (col <= nx - 8);
-    const bool e1 = (col + 1 <= nx - 8);
-    const bool e2 = (col + 2 <= nx - 8);
-    const bool e3 = (col + 3 <= nx - 8);
-    const int g_first = 1 - g.j0, g_last = g.ny - 2 - g.j0, g_top = g.ny - 1 - g.j0;
-    const int g_zero = -g.j0;
+    }
 
-    // one sweep of one row from the window (B, C, Tp) of the previous stage
-    auto stage = [&](const float4 &B, const float4 &Cc, const float4 &Tp,
-                     const float4 &Rh) -> float4 {
+    // one reference sweep of one row (model.rs:775-793 + BCs :807-815 per column)
+    __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
+                                            const float4 &Rh) const {
         const float L0 = __shfl_up(Cc.w, 1, 64);
         const float R3 = __shfl_down(Cc.x, 1, 64);
         const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
@@ -515,6 +496,8 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
         const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
         const float bb[4] = {B.x, B.y, B.z, B.w};
         const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
+        const float omega = 0.75f;
+        const float om1 = 1.0f - omega;
         float n[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -527,52 +510,39 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
         if (ch == 0) o.x = n[1];
         if (ch == nch - 1) o.w = 0.0f;
         return o;
-    };
-
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 W[T][3];      // W[s] = stage-s rows (k-s-2, k-s-1, k-s); stage 0 = input
-    float4 RH[T];        // RH[s] = rhs row k-1-s
-#pragma unroll
-    for (int s = 0; s < T; ++s) {
-        W[s][0] = W[s][1] = W[s][2] = z4;
-        RH[s] = z4;
     }
-    const int k_first = r0 - T, k_last = r1 + T - 1;
-    float4 pfP0 = ld4(rs_p, k_first), pfR0 = ld4(rs_r, k_first - 1);
-    float4 pfP1 = ld4(rs_p, k_first + 1), pfR1 = ld4(rs_r, k_first);
-    float m = 0.0f;
-    for (int k = k_first; k <= k_last; ++k) {
-        const float4 inP = pfP0, inR = pfR0;
-        pfP0 = pfP1;
-        pfR0 = pfR1;
-        pfP1 = ld4(rs_p, k + 2);
-        pfR1 = ld4(rs_r, k + 1);
-        W[0][0] = W[0][1];
-        W[0][1] = W[0][2];
-        W[0][2] = inP;
-#pragma unroll
-        for (int s = T - 1; s >= 1; --s) RH[s] = RH[s - 1];
-        RH[0] = inR;
+
+    // Slot v of the segment.  V is a compile-time value with V == v (mod 6)
+    // that fixes every ring index; in the warm-up (GUARD == 0, V == v
+    // exactly) it also decides at compile time which stages already have
+    // rows to compute (stage s starts at slot 2s).  GUARD == 2 is the final
+    // partial group: slots past the segment end return (uniform branch).
+    template <int V, int GUARD>
+    __device__ __forceinline__ void slot(int v) {
+        if (GUARD == 2 && v >= S) return;
+        const int k = k_first + v;
+        W[0][V % 3] = PF[V % 2];                             // input row k
+        PF[V % 2] = ld4(rs_p, k + 2);                        // two slots ahead
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
+            if (GUARD == 0 && V < 2 * s) continue;            // compile-time
             const int r = k - s;
-            if (k < r0 - T + 2 * s) continue;              // row not needed yet
-            float4 n = stage(W[s - 1][0], W[s - 1][1], W[s - 1][2], RH[s - 1]);
+            const float4 &B = W[s - 1][(V + 1) % 3];          // stage s-1, row r-1
+            const float4 &C = W[s - 1][(V + 2) % 3];          //              row r
+            const float4 &Tp = W[s - 1][V % 3];               //              row r+1
+            const float4 &Rh = RH[(V - s + 1 + 6) % 6];       // rhs row r
+            float4 n = stage(B, C, Tp, Rh);
             if (s < T) {
-                if (r == g_top) n = W[s][2];               // P(i,ny-1) = P(i,ny-2)
-                W[s][0] = W[s][1];
-                W[s][1] = W[s][2];
-                W[s][2] = n;
-                if (r == g_first) W[s][1] = n;             // P(i,0) = P(i,1)
-            } else if (r >= r0 && r < r1) {
-                if (r >= 0 && r < nyl) {
-                    const float4 C = W[T - 1][1];
-                    if (out_lane) {
-                        if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                        if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                        if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                        if (e3) m = fmaxf(m, fabsf(n.w - C.w));
-                    }
+                if (r == g_top) n = W[s][(V + 2) % 3];        // P(i,ny-1) = P(i,ny-2)
+                W[s][V % 3] = n;
+                if (r == g_first) W[s][(V + 2) % 3] = n;      // P(i,0) = P(i,1)
+            } else {
+                // final stage, rows r0 <= r < r1 (v >= 2T, v < S)
+                if (r < nyl && r >= 0 && out_lane) {
+                    if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                    if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                    if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                    if (e3) m = fmaxf(m, fabsf(n.w - C.w));
                 }
                 if (out_lane) {
                     *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
@@ -583,9 +553,116 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
                 }
             }
         }
+        RH[(V + 2) % 6] = ld4(rs_r, k + 1);                   // rhs row k+1
     }
-    m = wave_max(m);
-    if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
+
+    template <int V>
+    __device__ __forceinline__ void warmup() {
+        if constexpr (V < 2 * T) {
+            slot<V, 0>(V);
+            warmup<V + 1>();
+        }
+    }
+
+    // steady-state group of 6 slots starting at v = base (base == 2T mod 6)
+    template <int GUARD>
+    __device__ __forceinline__ void group(int base) {
+        slot<2 * T + 0, GUARD>(base + 0);
+        slot<2 * T + 1, GUARD>(base + 1);
+        slot<2 * T + 2, GUARD>(base + 2);
+        slot<2 * T + 3, GUARD>(base + 3);
+        slot<2 * T + 4, GUARD>(base + 4);
+        slot<2 * T + 5, GUARD>(base + 5);
+    }
+};
+
+// T weighted-Jacobi sweeps in one launch (temporal blocking; fixed-count
+// solves only — the tolerance test needs every sweep's residual).
+//
+// A wave owns 64 float4 column chunks; lanes 0 and 63 are halo lanes whose
+// values go stale one element per sweep from the outside in, so for T <= 4
+// lanes 1..62 (248 columns) stay exact and are the only ones stored; wave
+// columns overlap by two chunks.  The wave marches a segment of R output rows
+// through T pipelined stages: at row slot k it loads input row k and stage s
+// (1..T) computes row k-s from stage s-1's window of rows k-s-1..k-s+1, so
+// every stage is one sweep of the reference, at R + 2T row slots per segment.
+// p' and rhs come from HBM once per launch (12 B per T cell-updates).
+//
+// Per stage the p' boundary conditions of model.rs:807-815 are applied to the
+// window itself: column 0 takes column 1, column nx-1 is 0, global row ny-1
+// copies row ny-2, and global row 0 is patched with row 1 as soon as row 1 is
+// computed (before the next stage reads it).  Only the final stage is stored,
+// with the same fused boundary stores as k_jacobi.
+template <int T, int FAST>
+__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int R) {
+    if (pass_off(ctl, pass)) return;
+    TbWave<T, FAST> w;
+    // the wave index is uniform; readfirstlane lets the compiler see it, so
+    // every row/slot condition below becomes a scalar branch
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    w.lane = (int)threadIdx.x & 63;
+    const int wc = (int)blockIdx.x % nwc;
+    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
+    w.r0 = out_lo + seg * R;
+    w.r1 = min(w.r0 + R, out_hi);
+    if (w.r0 >= w.r1) return;
+    w.nx = g.nx;
+    w.nch = g.nx >> 2;
+    w.hg = g.hg;
+    w.nyl = g.nyl;
+    w.ch = wc * 62 - 1 + w.lane;
+    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
+    w.out_lane = in_dom && w.lane >= 1 && w.lane <= 62;
+
+    // buffers ping-pong once per LAUNCH: par = launches since the solve began
+    const int si = (ctl->cur + par) & 1;
+    float *src_alloc = si ? pb : pa;
+    float *dst_alloc = si ? pa : pb;
+    const int pbytes = (w.nyl + 2 * w.hg) * w.nx * 4;
+    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
+    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)w.hg * w.nx), 0, pbytes,
+                                               0x00020000);
+    w.dst = dst_alloc + (long)w.hg * w.nx;
+    w.dx_sq = g.dx_sq;
+    w.dy_sq = g.dy_sq;
+    w.denom = g.denom;
+    w.r_dx_sq = g.r_dx_sq;
+    w.r_dy_sq = g.r_dy_sq;
+    w.r_denom = g.r_denom;
+    w.col = 4 * w.ch;
+    w.row_bytes = w.nx * 4;
+    w.off0 = in_dom ? (w.hg * w.nx + w.col) * 4 : -16;
+    w.e0 = (w.col >= 1) && (w.col <= w.nx - 8);
+    w.e1 = (w.col + 1 <= w.nx - 8);
+    w.e2 = (w.col + 2 <= w.nx - 8);
+    w.e3 = (w.col + 3 <= w.nx - 8);
+    w.g_first = 1 - g.j0;
+    w.g_last = g.ny - 2 - g.j0;
+    w.g_top = g.ny - 1 - g.j0;
+    w.g_zero = -g.j0;
+    w.m = 0.0f;
+    w.k_first = w.r0 - T;
+    w.S = (w.r1 - w.r0) + 2 * T;
+
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < T; ++s) w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
+    // prologue loads: input rows k_first, k_first+1; rhs rows k_first-1, k_first
+    w.PF[0] = w.ld4(w.rs_p, w.k_first);
+    w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
+    w.RH[0] = w.ld4(w.rs_r, w.k_first - 1);
+    w.RH[1] = w.ld4(w.rs_r, w.k_first);
+#pragma unroll
+    for (int q = 2; q < 6; ++q) w.RH[q] = z4;
+    w.template warmup<0>();                        // slots 0 .. 2T-1
+    int base = 2 * T;
+    const int full_end = 2 * T + ((w.S - 2 * T) / 6) * 6;
+    for (; base < full_end; base += 6) w.template group<1>(base);
+    if (base < w.S) w.template group<2>(base);     // final partial group
+    const float m = wave_max(w.m);
+    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
 // End of a pressure solve: how many sweeps ran, which buffer is current, the
@@ -849,18 +926,19 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par,
                       int out_hi, hipStream_t s) {
     const int nch = g.nx / 4;
     const int nwc = cdiv(nch, 62);
-    const int nseg = cdiv(out_hi - out_lo, kTbRowsPerWave);
+    const int R = g.tb_rows > 0 ? g.tb_rows : kTbRowsPerWave;
+    const int nseg = cdiv(out_hi - out_lo, R);
     const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     if (g.fastdiv == 1)
-        hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 1>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc);
+        hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb,
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);
     else if (g.fastdiv == 2)
-        hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 2>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc);
+        hipLaunchKernelGGL((k_jacobi_tb<T, 2>), grid, block, 0, s, g, pa, pb,
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);
     else
-        hipLaunchKernelGGL((k_jacobi_tb<T, kTbRowsPerWave, 0>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc);
+        hipLaunchKernelGGL((k_jacobi_tb<T, 0>), grid, block, 0, s, g, pa, pb,
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);
 }
 
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
