@@ -31,6 +31,18 @@ __device__ __forceinline__ float wave_max(float m) {
     return m;
 }
 
+// Lane shifts on the VALU (DPP wave_shr:1 / wave_shl:1, gfx9 family) instead
+// of the LDS crossbar: lane l receives lane l-1 (from_left) or l+1
+// (from_right); the wave's end lanes receive 0 (they are halo lanes).
+__device__ __forceinline__ float from_left(float x) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float from_right(float x) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, false));
+}
+
 // x / c with the reference's IEEE rounding.  FAST 1 and 2 are used only for
 // divisors whose result equals IEEE `/` for every one of the 2^32 inputs,
 // proven on the device at model creation (verify_division, cfd_model.hip).
@@ -486,10 +498,11 @@ struct TbWave {
     }
 
     // one reference sweep of one row (model.rs:775-793 + BCs :807-815 per column)
+    template <bool EDGE>
     __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
                                             const float4 &Rh) const {
-        const float L0 = __shfl_up(Cc.w, 1, 64);
-        const float R3 = __shfl_down(Cc.x, 1, 64);
+        const float L0 = from_left(Cc.w);
+        const float R3 = from_right(Cc.x);
         const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
         const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
         const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
@@ -507,8 +520,10 @@ struct TbWave {
             n[k] = omega * p_update + om1 * cc[k];
         }
         float4 o = make_float4(n[0], n[1], n[2], n[3]);
-        if (ch == 0) o.x = n[1];
-        if (ch == nch - 1) o.w = 0.0f;
+        if (EDGE) {
+            if (ch == 0) o.x = n[1];
+            if (ch == nch - 1) o.w = 0.0f;
+        }
         return o;
     }
 
@@ -517,7 +532,7 @@ struct TbWave {
     // exactly) it also decides at compile time which stages already have
     // rows to compute (stage s starts at slot 2s).  GUARD == 2 is the final
     // partial group: slots past the segment end return (uniform branch).
-    template <int V, int GUARD>
+    template <int V, int GUARD, bool EDGE>
     __device__ __forceinline__ void slot(int v) {
         if (GUARD == 2 && v >= S) return;
         const int k = k_first + v;
@@ -531,11 +546,11 @@ struct TbWave {
             const float4 &C = W[s - 1][(V + 2) % 3];          //              row r
             const float4 &Tp = W[s - 1][V % 3];               //              row r+1
             const float4 &Rh = RH[(V - s + 1 + 6) % 6];       // rhs row r
-            float4 n = stage(B, C, Tp, Rh);
+            float4 n = stage<EDGE>(B, C, Tp, Rh);
             if (s < T) {
-                if (r == g_top) n = W[s][(V + 2) % 3];        // P(i,ny-1) = P(i,ny-2)
+                if (EDGE && r == g_top) n = W[s][(V + 2) % 3];   // P(i,ny-1) = P(i,ny-2)
                 W[s][V % 3] = n;
-                if (r == g_first) W[s][(V + 2) % 3] = n;      // P(i,0) = P(i,1)
+                if (EDGE && r == g_first) W[s][(V + 2) % 3] = n; // P(i,0) = P(i,1)
             } else {
                 // final stage, rows r0 <= r < r1 (v >= 2T, v < S)
                 if (r < nyl && r >= 0 && out_lane) {
@@ -546,9 +561,9 @@ struct TbWave {
                 }
                 if (out_lane) {
                     *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
-                    if (r == g_first)
+                    if (EDGE && r == g_first)
                         *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
-                    if (r == g_last)
+                    if (EDGE && r == g_last)
                         *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
                 }
             }
@@ -556,23 +571,35 @@ struct TbWave {
         RH[(V + 2) % 6] = ld4(rs_r, k + 1);                   // rhs row k+1
     }
 
-    template <int V>
+    template <int V, bool EDGE>
     __device__ __forceinline__ void warmup() {
         if constexpr (V < 2 * T) {
-            slot<V, 0>(V);
-            warmup<V + 1>();
+            slot<V, 0, EDGE>(V);
+            warmup<V + 1, EDGE>();
         }
     }
 
     // steady-state group of 6 slots starting at v = base (base == 2T mod 6)
-    template <int GUARD>
+    template <int GUARD, bool EDGE>
     __device__ __forceinline__ void group(int base) {
-        slot<2 * T + 0, GUARD>(base + 0);
-        slot<2 * T + 1, GUARD>(base + 1);
-        slot<2 * T + 2, GUARD>(base + 2);
-        slot<2 * T + 3, GUARD>(base + 3);
-        slot<2 * T + 4, GUARD>(base + 4);
-        slot<2 * T + 5, GUARD>(base + 5);
+        slot<2 * T + 0, GUARD, EDGE>(base + 0);
+        slot<2 * T + 1, GUARD, EDGE>(base + 1);
+        slot<2 * T + 2, GUARD, EDGE>(base + 2);
+        slot<2 * T + 3, GUARD, EDGE>(base + 3);
+        slot<2 * T + 4, GUARD, EDGE>(base + 4);
+        slot<2 * T + 5, GUARD, EDGE>(base + 5);
+    }
+
+    // the whole segment; EDGE = the wave touches a domain boundary (column 0
+    // or nx-1, or a global row 0/1/ny-2/ny-1 in any stage) and needs the
+    // boundary-condition logic; interior waves skip it entirely
+    template <bool EDGE>
+    __device__ __forceinline__ void run() {
+        warmup<0, EDGE>();                              // slots 0 .. 2T-1
+        int base = 2 * T;
+        const int full_end = 2 * T + ((S - 2 * T) / 6) * 6;
+        for (; base < full_end; base += 6) group<1, EDGE>(base);
+        if (base < S) group<2, EDGE>(base);             // final partial group
     }
 };
 
@@ -656,11 +683,14 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     w.RH[1] = w.ld4(w.rs_r, w.k_first);
 #pragma unroll
     for (int q = 2; q < 6; ++q) w.RH[q] = z4;
-    w.template warmup<0>();                        // slots 0 .. 2T-1
-    int base = 2 * T;
-    const int full_end = 2 * T + ((w.S - 2 * T) / 6) * 6;
-    for (; base < full_end; base += 6) w.template group<1>(base);
-    if (base < w.S) w.template group<2>(base);     // final partial group
+    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 1);
+    const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;   // every row any stage touches
+    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
+    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
+    if (col_edge || row_edge)
+        w.template run<true>();
+    else
+        w.template run<false>();
     const float m = wave_max(w.m);
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
