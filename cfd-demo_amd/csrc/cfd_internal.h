@@ -62,6 +62,7 @@ struct Geom {
     float r_dx_sq, r_dy_sq, r_denom;
     int32_t fastdiv;
     int32_t tb_rows;      // output rows per wave segment of k_jacobi_tb (0: default)
+    int32_t tb_kind;      // 1: k_jacobi_tb (chained stages), 2: k_jacobi_tb2 (skewed stages)
 };
 
 struct Fields {

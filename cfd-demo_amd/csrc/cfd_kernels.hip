@@ -695,6 +695,210 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
+// Skewed variant of k_jacobi_tb: stage s computes row k - 2s at slot k, so it
+// reads only rows its predecessor finished in EARLIER slots; the T stages of a
+// slot are independent and the compiler can interleave them (instruction-level
+// parallelism of T per wave instead of a T-long dependency chain).  Rings:
+//   W[s][pos(row)], pos(row) = (row - k_first) % 3       (stage s < T window)
+//   PF[v % 3]   p' input row k_first+v, loaded three slots ahead
+//   RH[(q - k_first + 1) % 12]  rhs row q (rows k-2T .. k+1 live)
+// The slot loop is unrolled by 12 = lcm(3, 3, 12); stages are processed
+// T..1 within a slot (reads before the predecessor overwrites its oldest row).
+template <int T, int FAST>
+struct TbSkew {
+    float4 W[T][3];
+    float4 RH[12];
+    float4 PF[3];
+    int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
+    int ch, col, lane, off0;
+    bool out_lane, e0, e1, e2, e3;
+    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
+    __amdgpu_buffer_rsrc_t rs_p, rs_r;
+    float *dst;
+    float m;
+
+    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int row) const {
+        constexpr int kOOB = -16;
+        const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                           __uint_as_float(v.w));
+    }
+
+    template <bool EDGE>
+    __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
+                                            const float4 &Rh) const {
+        const float L0 = from_left(Cc.w);
+        const float R3 = from_right(Cc.x);
+        const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
+        const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
+        const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
+        const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
+        const float bb[4] = {B.x, B.y, B.z, B.w};
+        const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
+        const float omega = 0.75f;
+        const float om1 = 1.0f - omega;
+        float n[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
+            const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
+            const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
+            n[k] = omega * p_update + om1 * cc[k];
+        }
+        float4 o = make_float4(n[0], n[1], n[2], n[3]);
+        if (EDGE) {
+            if (ch == 0) o.x = n[1];
+            if (ch == nch - 1) o.w = 0.0f;
+        }
+        return o;
+    }
+
+    static constexpr int md(int a, int b) { return ((a % b) + b) % b; }
+
+    // slot v; V == v (mod 12) fixes ring indices; WARM: V == v exactly and
+    // stage s runs only from slot 3s; GUARD: slots past S return
+    template <int V, bool WARM, bool GUARD, bool EDGE>
+    __device__ __forceinline__ void slot(int v) {
+        if (GUARD && v >= S) return;
+        const int k = k_first + v;
+        float4 nw[T + 1];
+#pragma unroll
+        for (int s = T; s >= 1; --s) {
+            if (WARM && V < 3 * s) continue;                   // compile-time
+            const int r = k - 2 * s;
+            const float4 &B = W[s - 1][md(V - 2 * s - 1, 3)];   // stage s-1, row r-1
+            const float4 &C = W[s - 1][md(V - 2 * s, 3)];       //              row r
+            const float4 &Tp = W[s - 1][md(V - 2 * s + 1, 3)];  //              row r+1
+            const float4 &Rh = RH[md(V - 2 * s + 1, 12)];       // rhs row r
+            float4 n = stage<EDGE>(B, C, Tp, Rh);
+            if (s < T) {
+                if (EDGE && r == g_top) n = W[s][md(V - 2 * s - 1, 3)];   // = row ny-2
+                nw[s] = n;
+            } else {
+                if (r < nyl && r >= 0 && out_lane) {
+                    if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                    if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                    if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                    if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                }
+                if (out_lane && (WARM || r < r1)) {
+                    *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
+                    if (EDGE && r == g_first)
+                        *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
+                    if (EDGE && r == g_last)
+                        *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
+                }
+            }
+        }
+        // commit the new rows (after every stage of this slot read its inputs)
+#pragma unroll
+        for (int s = 1; s < T; ++s) {
+            if (WARM && V < 3 * s) continue;
+            W[s][md(V - 2 * s, 3)] = nw[s];
+            if (EDGE && (k - 2 * s) == g_first) W[s][md(V - 2 * s - 1, 3)] = nw[s];  // row 0
+        }
+        W[0][md(V, 3)] = PF[md(V, 3)];                          // input row k
+        PF[md(V, 3)] = ld4(rs_p, k + 3);
+        RH[md(V + 2, 12)] = ld4(rs_r, k + 1);
+    }
+
+    template <int V, bool EDGE>
+    __device__ __forceinline__ void warmup() {
+        if constexpr (V < 3 * T) {
+            slot<V, true, false, EDGE>(V);
+            warmup<V + 1, EDGE>();
+        }
+    }
+
+    template <int U, bool GUARD, bool EDGE>
+    __device__ __forceinline__ void group12(int base) {
+        if constexpr (U < 12) {
+            slot<3 * T + U, false, GUARD, EDGE>(base + U);
+            group12<U + 1, GUARD, EDGE>(base);
+        }
+    }
+
+    template <bool EDGE>
+    __device__ __forceinline__ void run() {
+        warmup<0, EDGE>();                               // slots 0 .. 3T-1
+        int base = 3 * T;
+        const int full_end = 3 * T + ((S - 3 * T) / 12) * 12;
+        for (; base < full_end; base += 12) group12<0, false, EDGE>(base);
+        if (base < S) group12<0, true, EDGE>(base);
+    }
+};
+
+template <int T, int FAST>
+__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb2(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int R) {
+    if (pass_off(ctl, pass)) return;
+    TbSkew<T, FAST> w;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    w.lane = (int)threadIdx.x & 63;
+    const int wc = (int)blockIdx.x % nwc;
+    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
+    w.r0 = out_lo + seg * R;
+    w.r1 = min(w.r0 + R, out_hi);
+    if (w.r0 >= w.r1) return;
+    w.nx = g.nx;
+    w.nch = g.nx >> 2;
+    w.hg = g.hg;
+    w.nyl = g.nyl;
+    w.ch = wc * 62 - 1 + w.lane;
+    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
+    w.out_lane = in_dom && w.lane >= 1 && w.lane <= 62;
+    const int si = (ctl->cur + par) & 1;
+    float *src_alloc = si ? pb : pa;
+    float *dst_alloc = si ? pa : pb;
+    const int pbytes = (w.nyl + 2 * w.hg) * w.nx * 4;
+    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
+    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)w.hg * w.nx), 0, pbytes,
+                                               0x00020000);
+    w.dst = dst_alloc + (long)w.hg * w.nx;
+    w.dx_sq = g.dx_sq;
+    w.dy_sq = g.dy_sq;
+    w.denom = g.denom;
+    w.r_dx_sq = g.r_dx_sq;
+    w.r_dy_sq = g.r_dy_sq;
+    w.r_denom = g.r_denom;
+    w.col = 4 * w.ch;
+    w.row_bytes = w.nx * 4;
+    w.off0 = in_dom ? (w.hg * w.nx + w.col) * 4 : -16;
+    w.e0 = (w.col >= 1) && (w.col <= w.nx - 8);
+    w.e1 = (w.col + 1 <= w.nx - 8);
+    w.e2 = (w.col + 2 <= w.nx - 8);
+    w.e3 = (w.col + 3 <= w.nx - 8);
+    w.g_first = 1 - g.j0;
+    w.g_last = g.ny - 2 - g.j0;
+    w.g_top = g.ny - 1 - g.j0;
+    w.g_zero = -g.j0;
+    w.m = 0.0f;
+    w.k_first = w.r0 - T;
+    w.S = (w.r1 - w.r0) + 3 * T;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < T; ++s) w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) w.RH[q] = z4;
+    w.PF[0] = w.ld4(w.rs_p, w.k_first);
+    w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
+    w.PF[2] = w.ld4(w.rs_p, w.k_first + 2);
+    w.RH[0] = w.ld4(w.rs_r, w.k_first - 1);
+    w.RH[1] = w.ld4(w.rs_r, w.k_first);
+    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 1);
+    const int lo_row = w.k_first - 1, hi_row = w.k_first + w.S + 1;
+    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
+    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
+    if (col_edge || row_edge)
+        w.template run<true>();
+    else
+        w.template run<false>();
+    const float m = wave_max(w.m);
+    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
+}
+
 // End of a pressure solve: how many sweeps ran, which buffer is current, the
 // returned residual (model.rs:816-823), and whether the corrector loop goes on
 // (model.rs:721-723).  Resets the per-sweep slots for the next solve.
@@ -960,6 +1164,18 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par,
     const int nseg = cdiv(out_hi - out_lo, R);
     const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
+    if (g.tb_kind == 2) {
+        if (g.fastdiv == 1)
+            hipLaunchKernelGGL((k_jacobi_tb2<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
+                               pass, it, par, out_lo, out_hi, nwc, R);
+        else if (g.fastdiv == 2)
+            hipLaunchKernelGGL((k_jacobi_tb2<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
+                               pass, it, par, out_lo, out_hi, nwc, R);
+        else
+            hipLaunchKernelGGL((k_jacobi_tb2<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
+                               pass, it, par, out_lo, out_hi, nwc, R);
+        return;
+    }
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb,
                            f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);

@@ -536,6 +536,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, std::min(kMaxTemporal, atoi(tv)));
     g.tb_rows = kTbRowsPerWave;
     if (const char *rv = getenv("CFD_TB_ROWS")) g.tb_rows = std::max(4, std::min(1024, atoi(rv)));
+    g.tb_kind = 1;
+    if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = atoi(kv) == 2 ? 2 : 1;
 
     const size_t W = (size_t)nx + 1, nyl = (size_t)g.nyl;
     const size_t u_alloc = round4(m->u_rows_alloc() * W);

@@ -11,17 +11,18 @@ sys.path.insert(0, os.path.join(ROOT, "cfd-demo_amd"))
 import cfdamd  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-configs = [(t, r) for t in (1, 2, 3, 4) for r in (16, 32, 64, 128)]
+configs = [(k, t, r) for k in (1, 2) for t in (2, 3, 4) for r in (16, 24, 32, 48, 64)]
 grid = cfdamd.cavity_grid(n)
 params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
 models = {}
-for t, r in configs:
+for kind, t, r in configs:
+    os.environ["CFD_TB_KIND"] = str(kind)
     os.environ["CFD_TEMPORAL"] = str(t)
     os.environ["CFD_TB_ROWS"] = str(r)
     m = cfdamd.Model(grid, params)
     m.update_n(2)
     m.synchronize()
-    models[(t, r)] = m
+    models[(kind, t, r)] = m
 res = {c: [] for c in configs}
 for rnd in range(3):
     for c in configs:
@@ -33,6 +34,6 @@ for rnd in range(3):
 out = []
 for c in configs:
     us = statistics.median(res[c])
-    out.append({"T": c[0], "R": c[1], "us_per_sweep": us,
+    out.append({"kind": c[0], "T": c[1], "R": c[2], "us_per_sweep": us,
                 "cell_updates_per_s": n * n / (us * 1e-6)})
     print(json.dumps(out[-1]), flush=True)
