@@ -61,7 +61,9 @@ struct Geom {
     float dx_sq, dy_sq, denom;
     float r_dx_sq, r_dy_sq, r_denom;
     int32_t fastdiv;
-    int32_t tb_rows;      // output rows per wave segment of k_jacobi_tb (0: default)
+    int32_t tb_rows;      // fixed output rows per wave segment (0: balanced by tb_bpc)
+    int32_t tb_bpc;       // target k_jacobi_tb blocks per CU (balanced segmentation)
+    int32_t n_cu;         // compute units of the device
     int32_t tb_kind;      // 1: k_jacobi_tb (chained stages), 2: k_jacobi_tb2 (skewed stages)
 };
 

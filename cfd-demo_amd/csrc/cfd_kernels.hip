@@ -10,6 +10,8 @@
 // Citations are /root/reference/src/model.rs line numbers.
 #include "cfd_internal.h"
 
+#include <algorithm>
+
 namespace cfd {
 
 namespace {
@@ -623,7 +625,7 @@ struct TbWave {
 template <int T, int FAST>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int R) {
+    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
     if (pass_off(ctl, pass)) return;
     TbWave<T, FAST> w;
     // the wave index is uniform; readfirstlane lets the compiler see it, so
@@ -632,8 +634,11 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     w.lane = (int)threadIdx.x & 63;
     const int wc = (int)blockIdx.x % nwc;
     const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
-    w.r0 = out_lo + seg * R;
-    w.r1 = min(w.r0 + R, out_hi);
+    // balanced segments: nseg row ranges differing by at most one row
+    const int nrows = out_hi - out_lo;
+    if (seg >= nseg) return;
+    w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
+    w.r1 = out_lo + (int)(((long)(seg + 1) * nrows) / nseg);
     if (w.r0 >= w.r1) return;
     w.nx = g.nx;
     w.nch = g.nx >> 2;
@@ -832,15 +837,18 @@ struct TbSkew {
 template <int T, int FAST>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb2(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int R) {
+    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
     if (pass_off(ctl, pass)) return;
     TbSkew<T, FAST> w;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     w.lane = (int)threadIdx.x & 63;
     const int wc = (int)blockIdx.x % nwc;
     const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
-    w.r0 = out_lo + seg * R;
-    w.r1 = min(w.r0 + R, out_hi);
+    // balanced segments: nseg row ranges differing by at most one row
+    const int nrows = out_hi - out_lo;
+    if (seg >= nseg) return;
+    w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
+    w.r1 = out_lo + (int)(((long)(seg + 1) * nrows) / nseg);
     if (w.r0 >= w.r1) return;
     w.nx = g.nx;
     w.nch = g.nx >> 2;
@@ -1160,31 +1168,42 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par,
                       int out_hi, hipStream_t s) {
     const int nch = g.nx / 4;
     const int nwc = cdiv(nch, 62);
-    const int R = g.tb_rows > 0 ? g.tb_rows : kTbRowsPerWave;
-    const int nseg = cdiv(out_hi - out_lo, R);
+    // Segments per column strip: either fixed rows per wave (CFD_TB_ROWS) or
+    // enough balanced segments for ~tb_bpc blocks per CU, so the grid lands
+    // evenly on the CUs (an uneven block count left CUs idle: 544 blocks on
+    // 256 CUs ran at 71 % balance, 765 at ~100 %).
+    int nseg;
+    if (g.tb_rows > 0) {
+        nseg = cdiv(out_hi - out_lo, g.tb_rows);
+    } else {
+        const int blocks_per_strip = cdiv((long)g.tb_bpc * g.n_cu, nwc);
+        nseg = blocks_per_strip * kJacWavesPerBlock;
+        const int max_seg = (out_hi - out_lo) / 8;     // keep >= 8 rows per segment
+        if (nseg > max_seg) nseg = std::max(1, max_seg);
+    }
     const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     if (g.tb_kind == 2) {
         if (g.fastdiv == 1)
             hipLaunchKernelGGL((k_jacobi_tb2<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, R);
+                               pass, it, par, out_lo, out_hi, nwc, nseg);
         else if (g.fastdiv == 2)
             hipLaunchKernelGGL((k_jacobi_tb2<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, R);
+                               pass, it, par, out_lo, out_hi, nwc, nseg);
         else
             hipLaunchKernelGGL((k_jacobi_tb2<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, R);
+                               pass, it, par, out_lo, out_hi, nwc, nseg);
         return;
     }
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
     else if (g.fastdiv == 2)
         hipLaunchKernelGGL((k_jacobi_tb<T, 2>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
     else
         hipLaunchKernelGGL((k_jacobi_tb<T, 0>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, R);
+                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
 }
 
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,

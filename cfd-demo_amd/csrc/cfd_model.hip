@@ -534,8 +534,17 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         if (rc0) return rc0;
     }
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, std::min(kMaxTemporal, atoi(tv)));
-    g.tb_rows = kTbRowsPerWave;
+    g.tb_rows = 0;
     if (const char *rv = getenv("CFD_TB_ROWS")) g.tb_rows = std::max(4, std::min(1024, atoi(rv)));
+    g.tb_bpc = 3;
+    if (const char *bv = getenv("CFD_TB_BPC")) g.tb_bpc = std::max(1, std::min(16, atoi(bv)));
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            ncu <= 0)
+            ncu = 256;
+        g.n_cu = ncu;
+    }
     g.tb_kind = 1;
     if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = atoi(kv) == 2 ? 2 : 1;
 
@@ -646,10 +655,14 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     plan_slab(grid->ny, n_ranks, rank, &m->j0, &m->j1);
     int hg = 1;
     if (n_ranks > 1) {
-        const char *env = getenv("CFD_HALO_DEPTH");
-        hg = env ? atoi(env) : 8;
-        if (hg < 1) hg = 1;
+        // Deep halos: one RCCL round every hg sweeps (a round over xGMI is
+        // latency-bound, ~20-30 us) against ~hg/nyl redundant ghost-row
+        // compute; default hg = nyl/32 clamped to [4, 32] (32 at the bench's
+        // 1024-2048-row slabs: 7 rounds per 200-sweep step, ~3 % extra rows).
         uint64_t min_rows = grid->ny / (uint64_t)n_ranks;
+        const char *env = getenv("CFD_HALO_DEPTH");
+        hg = env ? atoi(env) : (int)std::max<uint64_t>(4, std::min<uint64_t>(32, min_rows / 32));
+        if (hg < 1) hg = 1;
         if ((uint64_t)hg + 2 > min_rows) hg = (int)(min_rows > 3 ? min_rows - 2 : 1);
         if (min_rows < 4) {
             delete m;

@@ -11,14 +11,21 @@ sys.path.insert(0, os.path.join(ROOT, "cfd-demo_amd"))
 import cfdamd  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-configs = [(k, t, r) for k in (1, 2) for t in (2, 3, 4) for r in (16, 24, 32, 48, 64)]
+# r > 0: fixed rows per wave; r < 0: balanced segmentation with -r blocks per CU
+configs = [(1, 4, r) for r in (20, 22, 24, 26, 28, 32, -2, -3, -4, -5, -6)] + \
+          [(1, 3, r) for r in (24, -3, -4)] + [(2, 4, r) for r in (24, -2, -3)]
 grid = cfdamd.cavity_grid(n)
 params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
 models = {}
 for kind, t, r in configs:
     os.environ["CFD_TB_KIND"] = str(kind)
     os.environ["CFD_TEMPORAL"] = str(t)
-    os.environ["CFD_TB_ROWS"] = str(r)
+    if r > 0:
+        os.environ["CFD_TB_ROWS"] = str(r)
+        os.environ.pop("CFD_TB_BPC", None)
+    else:
+        os.environ.pop("CFD_TB_ROWS", None)
+        os.environ["CFD_TB_BPC"] = str(-r)
     m = cfdamd.Model(grid, params)
     m.update_n(2)
     m.synchronize()
