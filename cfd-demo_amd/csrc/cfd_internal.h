@@ -112,7 +112,7 @@ void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 
 // Jacobi kernel geometry (exported for the roofline bookkeeping in bench).
 constexpr int kJacRowsPerWave = 16;
-constexpr int kMaxTemporal = 4;     // sweeps per temporally blocked launch
+constexpr int kMaxTemporal = 8;     // sweeps per temporally blocked launch (kind 3; 4 otherwise)
 constexpr int kTbRowsPerWave = 32;  // output rows per wave segment (TB kernel)
 constexpr int kJacWavesPerBlock = 4;
 

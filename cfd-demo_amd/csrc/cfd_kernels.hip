@@ -700,6 +700,203 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
+// Deep temporal blocking (T up to 8): the k_jacobi_tb register march with H
+// halo lanes on each side of the wave (edge values go stale one element per
+// sweep, so H = ceil(T/4) lanes; 64-2H lanes are stored) and the rhs rows
+// carried down the stages in a shift register (stage s at slot k uses rhs row
+// k-s, which stage s-1 used one slot earlier), so only the period-2 prefetch
+// and the period-3 windows index rings and the slot loop unrolls by 6.
+template <int T, int FAST>
+struct TbDeep {
+    static constexpr int H = (T + 3) / 4;
+    static constexpr int OUTL = 64 - 2 * H;
+    float4 W[T][3];
+    float4 RH[T];        // RH[s] = rhs row k-1-s at slot k (before the shift)
+    float4 PF[2];
+    int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
+    int ch, col, lane, off0;
+    bool out_lane, e0, e1, e2, e3;
+    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
+    __amdgpu_buffer_rsrc_t rs_p, rs_r;
+    float *dst;
+    float m;
+
+    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int row) const {
+        constexpr int kOOB = -16;
+        const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                           __uint_as_float(v.w));
+    }
+
+    template <bool EDGE>
+    __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
+                                            const float4 &Rh) const {
+        const float L0 = from_left(Cc.w);
+        const float R3 = from_right(Cc.x);
+        const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
+        const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
+        const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
+        const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
+        const float bb[4] = {B.x, B.y, B.z, B.w};
+        const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
+        const float omega = 0.75f;
+        const float om1 = 1.0f - omega;
+        float n[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
+            const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
+            const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
+            n[k] = omega * p_update + om1 * cc[k];
+        }
+        float4 o = make_float4(n[0], n[1], n[2], n[3]);
+        if (EDGE) {
+            if (ch == 0) o.x = n[1];
+            if (ch == nch - 1) o.w = 0.0f;
+        }
+        return o;
+    }
+
+    template <int V, int GUARD, bool EDGE>
+    __device__ __forceinline__ void slot(int v) {
+        if (GUARD == 2 && v >= S) return;
+        const int k = k_first + v;
+        W[0][V % 3] = PF[V % 2];
+        PF[V % 2] = ld4(rs_p, k + 2);
+        // rhs: stage s now needs row k-s, i.e. what stage s-1 had last slot
+#pragma unroll
+        for (int s = T - 1; s >= 1; --s) RH[s] = RH[s - 1];
+        RH[0] = ld4(rs_r, k - 1);
+#pragma unroll
+        for (int s = 1; s <= T; ++s) {
+            if (GUARD == 0 && V < 2 * s) continue;
+            const int r = k - s;
+            const float4 &B = W[s - 1][(V + 1) % 3];
+            const float4 &C = W[s - 1][(V + 2) % 3];
+            const float4 &Tp = W[s - 1][V % 3];
+            float4 n = stage<EDGE>(B, C, Tp, RH[s - 1]);
+            if (s < T) {
+                if (EDGE && r == g_top) n = W[s][(V + 2) % 3];
+                W[s][V % 3] = n;
+                if (EDGE && r == g_first) W[s][(V + 2) % 3] = n;
+            } else {
+                if (r < nyl && r >= 0 && out_lane) {
+                    if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                    if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                    if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                    if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                }
+                if (out_lane) {
+                    *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
+                    if (EDGE && r == g_first)
+                        *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
+                    if (EDGE && r == g_last)
+                        *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
+                }
+            }
+        }
+    }
+
+    template <int V, bool EDGE>
+    __device__ __forceinline__ void warmup() {
+        if constexpr (V < 2 * T) {
+            slot<V, 0, EDGE>(V);
+            warmup<V + 1, EDGE>();
+        }
+    }
+
+    template <int GUARD, bool EDGE>
+    __device__ __forceinline__ void group(int base) {
+        slot<2 * T + 0, GUARD, EDGE>(base + 0);
+        slot<2 * T + 1, GUARD, EDGE>(base + 1);
+        slot<2 * T + 2, GUARD, EDGE>(base + 2);
+        slot<2 * T + 3, GUARD, EDGE>(base + 3);
+        slot<2 * T + 4, GUARD, EDGE>(base + 4);
+        slot<2 * T + 5, GUARD, EDGE>(base + 5);
+    }
+
+    template <bool EDGE>
+    __device__ __forceinline__ void run() {
+        warmup<0, EDGE>();
+        int base = 2 * T;
+        const int full_end = 2 * T + ((S - 2 * T) / 6) * 6;
+        for (; base < full_end; base += 6) group<1, EDGE>(base);
+        if (base < S) group<2, EDGE>(base);
+    }
+};
+
+template <int T, int FAST>
+__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
+    if (pass_off(ctl, pass)) return;
+    using Wv = TbDeep<T, FAST>;
+    Wv w;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    w.lane = (int)threadIdx.x & 63;
+    const int wc = (int)blockIdx.x % nwc;
+    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
+    const int nrows = out_hi - out_lo;
+    if (seg >= nseg) return;
+    w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
+    w.r1 = out_lo + (int)(((long)(seg + 1) * nrows) / nseg);
+    if (w.r0 >= w.r1) return;
+    w.nx = g.nx;
+    w.nch = g.nx >> 2;
+    w.hg = g.hg;
+    w.nyl = g.nyl;
+    w.ch = wc * Wv::OUTL - Wv::H + w.lane;
+    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
+    w.out_lane = in_dom && w.lane >= Wv::H && w.lane < 64 - Wv::H;
+    const int si = (ctl->cur + par) & 1;
+    float *src_alloc = si ? pb : pa;
+    float *dst_alloc = si ? pa : pb;
+    const int pbytes = (w.nyl + 2 * w.hg) * w.nx * 4;
+    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
+    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)w.hg * w.nx), 0, pbytes,
+                                               0x00020000);
+    w.dst = dst_alloc + (long)w.hg * w.nx;
+    w.dx_sq = g.dx_sq;
+    w.dy_sq = g.dy_sq;
+    w.denom = g.denom;
+    w.r_dx_sq = g.r_dx_sq;
+    w.r_dy_sq = g.r_dy_sq;
+    w.r_denom = g.r_denom;
+    w.col = 4 * w.ch;
+    w.row_bytes = w.nx * 4;
+    w.off0 = in_dom ? (w.hg * w.nx + w.col) * 4 : -16;
+    w.e0 = (w.col >= 1) && (w.col <= w.nx - 8);
+    w.e1 = (w.col + 1 <= w.nx - 8);
+    w.e2 = (w.col + 2 <= w.nx - 8);
+    w.e3 = (w.col + 3 <= w.nx - 8);
+    w.g_first = 1 - g.j0;
+    w.g_last = g.ny - 2 - g.j0;
+    w.g_top = g.ny - 1 - g.j0;
+    w.g_zero = -g.j0;
+    w.m = 0.0f;
+    w.k_first = w.r0 - T;
+    w.S = (w.r1 - w.r0) + 2 * T;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < T; ++s) {
+        w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
+        w.RH[s] = z4;
+    }
+    w.PF[0] = w.ld4(w.rs_p, w.k_first);
+    w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
+    const bool col_edge = (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 1);
+    const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;
+    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
+    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
+    if (col_edge || row_edge)
+        w.template run<true>();
+    else
+        w.template run<false>();
+    const float m = wave_max(w.m);
+    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
+}
+
 // Skewed variant of k_jacobi_tb: stage s computes row k - 2s at slot k, so it
 // reads only rows its predecessor finished in EARLIER slots; the T stages of a
 // slot are independent and the compiler can interleave them (instruction-level
@@ -1167,7 +1364,8 @@ template <int T>
 static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par, int out_lo,
                       int out_hi, hipStream_t s) {
     const int nch = g.nx / 4;
-    const int nwc = cdiv(nch, 62);
+    const int outl = g.tb_kind == 3 ? 64 - 2 * ((T + 3) / 4) : 62;
+    const int nwc = cdiv(nch, outl);
     // Segments per column strip: either fixed rows per wave (CFD_TB_ROWS) or
     // enough balanced segments for ~tb_bpc blocks per CU, so the grid lands
     // evenly on the CUs (an uneven block count left CUs idle: 544 blocks on
@@ -1183,6 +1381,19 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par,
     }
     const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
+    if (g.tb_kind == 3) {
+        if (g.fastdiv == 1)
+            hipLaunchKernelGGL((k_jacobi_tb3<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
+                               pass, it, par, out_lo, out_hi, nwc, nseg);
+        else if (g.fastdiv == 2)
+            hipLaunchKernelGGL((k_jacobi_tb3<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
+                               pass, it, par, out_lo, out_hi, nwc, nseg);
+        else
+            hipLaunchKernelGGL((k_jacobi_tb3<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
+                               pass, it, par, out_lo, out_hi, nwc, nseg);
+        return;
+    }
+    if constexpr (T <= 4) {
     if (g.tb_kind == 2) {
         if (g.fastdiv == 1)
             hipLaunchKernelGGL((k_jacobi_tb2<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
@@ -1204,11 +1415,21 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par,
     else
         hipLaunchKernelGGL((k_jacobi_tb<T, 0>), grid, block, 0, s, g, pa, pb,
                            f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
+    }
 }
 
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
                          int out_lo, int out_hi, hipStream_t s) {
     if (out_hi <= out_lo) return;
+    if (T > 4 && g.tb_kind == 3) {
+        switch (T) {
+        case 5: launch_tb<5>(g, f, pass, it, par, out_lo, out_hi, s); break;
+        case 6: launch_tb<6>(g, f, pass, it, par, out_lo, out_hi, s); break;
+        case 7: launch_tb<7>(g, f, pass, it, par, out_lo, out_hi, s); break;
+        default: launch_tb<8>(g, f, pass, it, par, out_lo, out_hi, s); break;
+        }
+        return;
+    }
     switch (T) {
     case 1: launch_tb<1>(g, f, pass, it, par, out_lo, out_hi, s); break;
     case 2: launch_tb<2>(g, f, pass, it, par, out_lo, out_hi, s); break;

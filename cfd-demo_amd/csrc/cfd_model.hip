@@ -533,7 +533,11 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         int rc0 = choose_division(m->stream, g);
         if (rc0) return rc0;
     }
-    if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, std::min(kMaxTemporal, atoi(tv)));
+    g.tb_kind = 1;
+    if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = std::max(1, std::min(3, atoi(kv)));
+    m->t_max = g.tb_kind == 3 ? 8 : 4;
+    if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
+    m->t_max = std::min(m->t_max, g.tb_kind == 3 ? kMaxTemporal : 4);
     g.tb_rows = 0;
     if (const char *rv = getenv("CFD_TB_ROWS")) g.tb_rows = std::max(4, std::min(1024, atoi(rv)));
     g.tb_bpc = 3;
@@ -545,8 +549,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
             ncu = 256;
         g.n_cu = ncu;
     }
-    g.tb_kind = 1;
-    if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = atoi(kv) == 2 ? 2 : 1;
+
 
     const size_t W = (size_t)nx + 1, nyl = (size_t)g.nyl;
     const size_t u_alloc = round4(m->u_rows_alloc() * W);

@@ -12,8 +12,9 @@ import cfdamd  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 # r > 0: fixed rows per wave; r < 0: balanced segmentation with -r blocks per CU
-configs = [(1, 4, r) for r in (20, 22, 24, 26, 28, 32, -2, -3, -4, -5, -6)] + \
-          [(1, 3, r) for r in (24, -3, -4)] + [(2, 4, r) for r in (24, -2, -3)]
+configs = [(1, 4, r) for r in (24, -2, -3, -4, -5)] + \
+          [(3, 8, r) for r in (24, 32, 48, -1, -2, -3, -4)] + \
+          [(3, 6, r) for r in (-2, -3)] + [(3, 4, r) for r in (-3, -4)]
 grid = cfdamd.cavity_grid(n)
 params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
 models = {}
