@@ -81,7 +81,7 @@ struct Fields {
 
 // ---- launchers (cfd_kernels.hip) ----
 // pass < 0 means "not inside the corrector loop" (always runs).
-void launch_step_begin(const Geom &g, const Fields &f, hipStream_t s);
+void launch_step_begin(const Geom &g, const Fields &f, int copy, hipStream_t s);
 void launch_copy_star(const Geom &g, const Fields &f, int pass, hipStream_t s);
 void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
@@ -107,6 +107,7 @@ void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, 
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s);
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);
+void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s);
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 

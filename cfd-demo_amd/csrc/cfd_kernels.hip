@@ -97,11 +97,15 @@ __device__ __forceinline__ void copy4(float *__restrict__ dst, const float *__re
 }
 
 // update() prologue (model.rs:307-316): u_old <- u, v_old <- v, inlet ramp.
-__global__ __launch_bounds__(kBlock) void k_step_begin(Geom g, Fields f) {
+// With `copy` 0 (the fused corrector computes the residuals from the values it
+// overwrites) only the control words are touched.
+__global__ __launch_bounds__(kBlock) void k_step_begin(Geom g, Fields f, int copy) {
     const size_t tid = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    copy4(f.u_old_base, f.u_alloc_base, f.u_alloc / 4, tid, stride);
-    copy4(f.v_old_base, f.v_alloc_base, f.v_alloc / 4, tid, stride);
+    if (copy) {
+        copy4(f.u_old_base, f.u_alloc_base, f.u_alloc / 4, tid, stride);
+        copy4(f.v_old_base, f.v_alloc_base, f.v_alloc / 4, tid, stride);
+    }
     if (tid == 0) {
         Ctl *c = f.ctl;
         const uint32_t st = c->step;
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float 
     const float convective = (f_e - f_w) / dx + (f_n - f_s) / dy;
     const float laplace = (ue1 - 2.0f * uc + uw1) / (dx * dx) + (un1 - 2.0f * uc + us1) / (dy * dy);
     float r = uc + dt * (-convective + nu * laplace);
-    if (f.mask_u[(long)lj * W + i] == 1) r = 0.0f;
+    if (f.mask_u[(long)lj * W + i] & 1) r = 0.0f;
     f.u_star[c] = r;
 }
 
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float 
         }
     }
     float r;
-    if (f.mask_v[cv] == 1) {
+    if (f.mask_v[cv] & 1) {
         r = 0.0f;
     } else {
         const float dx = g.dx, dy = g.dy, nu = g.nu;
@@ -1176,6 +1180,17 @@ __global__ __launch_bounds__(kBlock) void k_corrector(Geom g, Fields f, int pass
 
 // ------------------------------------------------- velocity boundaries (K6)
 
+// Inlet face value of row j (model.rs:830-846): uniform or parabolic, >= 0.
+__device__ __forceinline__ float inlet_value(const Geom &g, float inlet, int j) {
+    if (g.profile == 0) return inlet;
+    const float y = ((float)j + 0.5f) * g.dy;
+    const float center = g.ly / 2.0f;
+    const float radius = g.ly / 2.0f;
+    const float q = (y - center) / radius;
+    const float pv = inlet * (1.0f - q * q);
+    return pv < 0.0f ? 0.0f : pv;
+}
+
 // apply_boundary_conditions (model.rs:826-875), in the reference's order; a
 // single workgroup with barriers between the phases that touch the same
 // faces.  bc_kind 1 = build-defined lid-driven cavity.
@@ -1188,18 +1203,7 @@ __global__ __launch_bounds__(1024) void k_boundary(Geom g, Fields f) {
     for (int lj = t; lj < nyl; lj += nt) {
         const int j = g.j0 + lj;
         if (g.bc_kind == 0) {
-            float val;
-            if (g.profile == 0) {
-                val = inlet;
-            } else {
-                const float y = ((float)j + 0.5f) * g.dy;
-                const float center = g.ly / 2.0f;
-                const float radius = g.ly / 2.0f;
-                const float q = (y - center) / radius;
-                const float pv = inlet * (1.0f - q * q);
-                val = pv < 0.0f ? 0.0f : pv;
-            }
-            u[(long)lj * W] = val;
+            u[(long)lj * W] = inlet_value(g, inlet, j);
             u[(long)lj * W + nx] = u[(long)lj * W + nx - 1];
         } else {
             u[(long)lj * W] = 0.0f;
@@ -1226,6 +1230,87 @@ __global__ __launch_bounds__(1024) void k_boundary(Geom g, Fields f) {
         const int lj = oj - g.j0;
         if (lj >= 0 && lj < nyl) u[(long)lj * W + oi] = 0.0f;
         if (lj >= 0 && lj <= nyl) v[(long)lj * nx + oi] = 0.0f;
+    }
+}
+
+// ------------------------------- fused corrector + boundaries + reductions (K5')
+
+// update() with no extra corrector passes (model.rs:707-730 with
+// corrector_passes 0): the one corrector pass (apply_corrector :1334-1404),
+// the velocity boundaries (apply_boundary_conditions :827-875) and the step
+// residuals/CFL maxima (:333-344, :879-880) in a single pass over the fields.
+// Each thread writes the FINAL value of its u face and v face — the value the
+// reference holds after the boundary routine has run in its order (columns,
+// then rows over the corners, then obstacle faces) — and, because u/v are not
+// touched between step start and here, the value it overwrites IS u_old/v_old:
+// |new - old| needs no copy of the old fields and no second read.  Obstacle
+// faces are bit 1 of the device masks.  Same grid as k_corrector.
+__global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, float dt_override,
+                                                           int nbx) {
+    Ctl *c = f.ctl;
+    const int i = (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
+    const int lj = (int)(blockIdx.x / nbx);                             // 0..nyl
+    const int nx = g.nx, W = nx + 1;
+    float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
+    if (i <= nx) {
+        const float dt = dt_of(c, dt_override);
+        const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+        const int j = g.j0 + lj;
+        const long rp = (long)lj * nx;
+        if (lj < g.nyl) {
+            const long k = (long)lj * W + i;
+            float nw;
+            if (j == 0) {
+                nw = 0.0f;
+            } else if (j == g.ny - 1) {
+                nw = (g.bc_kind == 1 && i > 0 && i < nx) ? c->inlet : 0.0f;
+            } else if (i == 0) {
+                nw = g.bc_kind == 0 ? inlet_value(g, c->inlet, j) : 0.0f;
+            } else if (i == nx) {
+                // outflow copies the corrected face nx-1 (scalar tail association, Q9)
+                nw = g.bc_kind == 0
+                         ? f.u_star[k - 1] - dt * (pp[rp + nx - 1] - pp[rp + nx - 2]) / g.dx
+                         : 0.0f;
+            } else {
+                const float p_right = pp[rp + i];
+                const float p_left = pp[rp + i - 1];
+                nw = (i >= nx - 7) ? f.u_star[k] - dt * (p_right - p_left) / g.dx
+                                   : f.u_star[k] - dt * ((p_right - p_left) / g.dx);
+            }
+            if (f.n_obs > 0 && (f.mask_u[k] & 2)) nw = 0.0f;
+            const float old = f.u[k];
+            f.u[k] = nw;
+            du = fmaxf(0.f, fabsf(nw - old));
+            mu = fmaxf(0.f, fabsf(nw));
+        }
+        if (i < nx) {
+            const long k = rp + i;
+            float nw;
+            if (j == 0 || j == g.ny) {
+                nw = 0.0f;
+            } else {
+                const float p_top = pp[k];
+                const float p_bottom = pp[k - nx];
+                nw = f.v_star[k] - dt * ((p_top - p_bottom) / g.dy);
+            }
+            if (f.n_obs > 0 && (f.mask_v[k] & 2)) nw = 0.0f;
+            const float old = f.v[k];
+            f.v[k] = nw;
+            dv = fmaxf(0.f, fabsf(nw - old));
+            mv = fmaxf(0.f, fabsf(nw));
+            if (lj < g.nyl) f.p[k] = f.p[k] + pp[k];
+        }
+    }
+    du = wave_max(du);
+    dv = wave_max(dv);
+    mu = wave_max(mu);
+    mv = wave_max(mv);
+    if ((threadIdx.x & 63) == 0) {
+        uint32_t *r = c->red;
+        if (du > 0.f) atomicMax(&r[0], __float_as_uint(du));
+        if (dv > 0.f) atomicMax(&r[1], __float_as_uint(dv));
+        if (mu > 0.f) atomicMax(&r[2], __float_as_uint(mu));
+        if (mv > 0.f) atomicMax(&r[3], __float_as_uint(mv));
     }
 }
 
@@ -1295,9 +1380,10 @@ inline int copy_grid(size_t n4) {
 
 // ------------------------------------------------------------------ launchers
 
-void launch_step_begin(const Geom &g, const Fields &f, hipStream_t s) {
+void launch_step_begin(const Geom &g, const Fields &f, int copy, hipStream_t s) {
     size_t n4 = f.u_alloc > f.v_alloc ? f.u_alloc / 4 : f.v_alloc / 4;
-    hipLaunchKernelGGL(k_step_begin, dim3(copy_grid(n4)), dim3(kBlock), 0, s, g, f);
+    hipLaunchKernelGGL(k_step_begin, dim3(copy ? copy_grid(n4) : 1), dim3(kBlock), 0, s, g, f,
+                       copy);
 }
 
 void launch_copy_star(const Geom &g, const Fields &f, int pass, hipStream_t s) {
@@ -1452,6 +1538,12 @@ void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_overrid
                       hipStream_t s) {
     const int nbx = cdiv(g.nx + 1, kBlock);
     hipLaunchKernelGGL(k_corrector, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,
+                       dt_override, nbx);
+}
+
+void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+    const int nbx = cdiv(g.nx + 1, kBlock);
+    hipLaunchKernelGGL(k_correct_finish, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f,
                        dt_override, nbx);
 }
 

@@ -99,6 +99,7 @@ struct cfd_model {
     int32_t *obs = nullptr;
     Ctl *ctl = nullptr;
     std::vector<uint8_t> h_mask_u, h_mask_v;
+    std::vector<uint8_t> dmask_u, dmask_v;   // staging for the async mask upload
     // sharding
     int n_ranks = 1, rank = 0;
     uint64_t j0 = 0, j1 = 0;
@@ -321,9 +322,19 @@ struct cfd_model {
     bool host_driven() const { return sharded() && params.tol_enabled; }
 
     // piso_step (model.rs:529-730).
-    int enqueue_piso(float dt_override) {
+    // finish = inside update() with no extra corrector passes: the corrector,
+    // the boundaries and the step reductions run as one fused pass.
+    int enqueue_piso(float dt_override, bool finish = false) {
         launch_u_predictor(g, f, dt_override, stream);
         launch_v_predictor(g, f, dt_override, stream);
+        if (finish) {
+            launch_divergence(g, f, host_driven() ? -1 : 0, dt_override, stream);
+            int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
+            if (rc) return rc;
+            launch_correct_finish(g, f, dt_override, stream);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
         if (!host_driven()) {
             launch_divergence(g, f, 0, dt_override, stream);
             int rc = enqueue_solve(0);
@@ -364,12 +375,13 @@ struct cfd_model {
             step_events.push_back(e0);
         }
         HIP_TRY(hipEventRecord(ev_step0, stream));
-        launch_step_begin(g, f, stream);
+        const bool fused = params.corrector_passes == 0;
+        launch_step_begin(g, f, fused ? 0 : 1, stream);
         int rc = exchange_uv();
         if (rc) return rc;
-        rc = enqueue_piso(kNaN);
+        rc = enqueue_piso(kNaN, fused);
         if (rc) return rc;
-        launch_step_reduce(g, f, stream);
+        if (!fused) launch_step_reduce(g, f, stream);
         rc = allreduce_max_u32(f.ctl->red, 4);
         if (rc) return rc;
         launch_step_finalize(g, f, stream);
@@ -599,8 +611,20 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     }
     m->h_mask_u = mu;
     m->h_mask_v = mv;
-    HIP_TRY(hipMemcpyAsync(m->mask_u, mu.data(), mu.size(), hipMemcpyHostToDevice, m->stream));
-    HIP_TRY(hipMemcpyAsync(m->mask_v, mv.data(), mv.size(), hipMemcpyHostToDevice, m->stream));
+    // device masks: bit 0 = predictor mask (model.rs:235-260), bit 1 = face
+    // zeroed by the obstacle loop of apply_boundary_conditions (:866-874)
+    std::vector<uint8_t> dmu(mu), dmv(mv);
+    for (size_t k = 0; k < obs.size(); k += 2) {
+        const long oi = obs[k], lj = (long)obs[k + 1] - (long)m->j0;
+        if (lj >= 0 && lj < (long)nyl) dmu[lj * W + oi] |= 2;
+        if (lj >= 0 && lj <= (long)nyl) dmv[lj * nx + oi] |= 2;
+    }
+    m->dmask_u = std::move(dmu);
+    m->dmask_v = std::move(dmv);
+    HIP_TRY(hipMemcpyAsync(m->mask_u, m->dmask_u.data(), m->dmask_u.size(), hipMemcpyHostToDevice,
+                           m->stream));
+    HIP_TRY(hipMemcpyAsync(m->mask_v, m->dmask_v.data(), m->dmask_v.size(), hipMemcpyHostToDevice,
+                           m->stream));
     if (!obs.empty()) {
         HIP_TRY(hipMalloc((void **)&m->obs, obs.size() * 4));
         HIP_TRY(hipMemcpyAsync(m->obs, obs.data(), obs.size() * 4, hipMemcpyHostToDevice, m->stream));

@@ -131,6 +131,28 @@ def test_live_oracle_channel_nonsquare(scheme):
     assert (r.simulation_step, np.float32(r.dt), np.float32(r.p)) == (s.step, np.float32(s.dt), np.float32(s.p))
 
 
+@pytest.mark.parametrize("scheme,profile,tol", [(0, 0, 1), (1, 1, 0), (0, 1, 0), (1, 0, 1)])
+def test_fused_finish_channel(scheme, profile, tol):
+    """corrector_passes 0 runs corrector + boundaries + step residuals as one fused
+    kernel (k_correct_finish): channel with the cylinder (outflow copy, obstacle
+    faces, uniform/parabolic inlet), residuals compared every step."""
+    c = _cfd()
+    g = dict(nx=192, ny=96, lx=30.0, ly=10.0, cylinder=(7.5, 5.0, 1.5))
+    kw = dict(scheme=scheme, inlet_profile=profile, jacobi_iters=40, corrector_passes=0,
+              tol_enabled=tol)
+    o = _oracle(g, **kw)
+    m = c.Model(_grid(g), _params(kw))
+    for step in range(8):
+        o.update()
+        m.update()
+        s, r = o.scalars(), m.get_residuals()
+        for a, b in ((s.u, r.u), (s.v, r.v), (s.p, r.p), (s.dt, r.dt)):
+            assert np.float32(a).view(np.uint32) == np.float32(b).view(np.uint32), step
+    st = m.get_state()
+    for f in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
+        assert_bitwise(f, st[f], o.field(f))
+
+
 def test_jacobi_tolerance_and_fixed_paths():
     """jacobi_pressure with random p'/rhs: early-exit (tol on) and fixed count."""
     c = _cfd()

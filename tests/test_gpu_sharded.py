@@ -81,6 +81,7 @@ def check_against_oracle(states, grid, oracle_kw, steps, fields):
         assert np.float32(st["dt"]) == np.float32(s.dt)
         assert np.float32(st["last_p_residual"]) == np.float32(s.p)
         assert np.float32(st["last_u_residual"]) == np.float32(s.u)
+        assert np.float32(st["last_v_residual"]) == np.float32(s.v)
         assert st["simulation_step"] == s.step
 
 
@@ -119,3 +120,19 @@ def test_sharded_bench_like_config():
     st = run_sharded(4, grid, params, 3, 8)
     check_against_oracle(st, grid, dict(bc_kind=1, viscosity=0.001, jacobi_iters=200,
                                         corrector_passes=0, tol_enabled=0), 3, FIELDS)
+
+
+@pytest.mark.parametrize("n,tol", [(2, False), (3, True)])
+def test_sharded_fused_finish_channel_cylinder(n, tol):
+    """No extra corrector passes: the fused corrector/boundary/residual kernel
+    on slabs, outflow + obstacle faces across the slab boundary, residual maxima
+    all-reduced; tolerance on takes the host-driven solve."""
+    import cfdamd
+    grid = cfdamd.Grid(128, 60, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.9))
+    params = cfdamd.SimulationParams(velocity_scheme=cfdamd.VelocityScheme(1),
+                                     inlet_profile=cfdamd.InletProfile(1), jacobi_iters=40,
+                                     corrector_passes=0, tol_enabled=tol)
+    st = run_sharded(n, grid, params, 5, 4)
+    check_against_oracle(st, grid, dict(scheme=1, inlet_profile=1, jacobi_iters=40,
+                                        corrector_passes=0, tol_enabled=int(tol)), 5,
+                         FIELDS + ("rhs",))

@@ -12,9 +12,11 @@ import cfdamd  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 # r > 0: fixed rows per wave; r < 0: balanced segmentation with -r blocks per CU
-configs = [(1, 4, r) for r in (24, -2, -3, -4, -5)] + \
-          [(3, 8, r) for r in (24, 32, 48, -1, -2, -3, -4)] + \
-          [(3, 6, r) for r in (-2, -3)] + [(3, 4, r) for r in (-3, -4)]
+configs = [(1, 4, r) for r in (12, 18, 24, 30, 36, 42, 32)] + \
+          [(3, 8, r) for r in (18, 24, 30, 36)] + [(3, 6, r) for r in (24, 30, 36)] + \
+          [(1, 3, r) for r in (24, 30)]
+if os.environ.get("TUNE_CONFIGS"):
+    configs = [tuple(int(x) for x in c.split(",")) for c in os.environ["TUNE_CONFIGS"].split(";")]
 grid = cfdamd.cavity_grid(n)
 params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
 models = {}
