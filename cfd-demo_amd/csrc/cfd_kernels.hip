@@ -35,14 +35,15 @@ __device__ __forceinline__ float wave_max(float m) {
 
 // Lane shifts on the VALU (DPP wave_shr:1 / wave_shl:1, gfx9 family) instead
 // of the LDS crossbar: lane l receives lane l-1 (from_left) or l+1
-// (from_right); the wave's end lanes receive 0 (they are halo lanes).
+// (from_right); the wave's end lanes receive 0 (bound_ctrl: no register
+// initialisation needed; they are halo lanes).
 __device__ __forceinline__ float from_left(float x) {
     return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, false));
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float from_right(float x) {
     return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, false));
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, true));
 }
 
 // x / c with the reference's IEEE rounding.  FAST 1 and 2 are used only for
@@ -57,6 +58,43 @@ __device__ __forceinline__ float fdiv(float x, float c, float r) {
         return __builtin_isfinite(q0) ? q : q0;
     }
     return x / c;
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int FAST>
+__device__ __forceinline__ f2 fdiv2(f2 x, float c, float r) {
+    if (FAST == 1) return x * r;                        // v_pk_mul_f32
+    return (f2){fdiv<FAST>(x.x, c, r), fdiv<FAST>(x.y, c, r)};
+}
+
+// One reference Jacobi update (model.rs:775-793) of the 4 consecutive
+// columns a lane holds, C = row j, B = row j-1, T = row j+1, Rh = rhs row j,
+// L0 / R3 = the columns left / right of the chunk.  The arithmetic is the
+// reference's, operation for operation, on column pairs: each pair is one
+// packed VOP3P instruction, and the horizontal sums are formed as
+// swap(C01) + (L0, C.z) and swap(C23) + (C.y, R3), so the swap folds into
+// op_sel and only two register moves remain per 4 columns (f32 addition is
+// commutative bit for bit).
+template <int FAST>
+__device__ __forceinline__ float4 jacobi_row4(const float4 &B, const float4 &C, const float4 &T,
+                                              const float4 &Rh, float L0, float R3, float dx_sq,
+                                              float dy_sq, float denom, float r_dx_sq,
+                                              float r_dy_sq, float r_denom) {
+    const f2 c01 = {C.x, C.y}, c23 = {C.z, C.w};
+    const f2 h01 = __builtin_shufflevector(c01, c01, 1, 0) + (f2){L0, C.z};
+    const f2 h23 = __builtin_shufflevector(c23, c23, 1, 0) + (f2){C.y, R3};
+    const f2 v01 = (f2){T.x, T.y} + (f2){B.x, B.y};
+    const f2 v23 = (f2){T.z, T.w} + (f2){B.z, B.w};
+    const f2 hz01 = fdiv2<FAST>(h01, dx_sq, r_dx_sq), hz23 = fdiv2<FAST>(h23, dx_sq, r_dx_sq);
+    const f2 vt01 = fdiv2<FAST>(v01, dy_sq, r_dy_sq), vt23 = fdiv2<FAST>(v23, dy_sq, r_dy_sq);
+    const f2 pu01 = fdiv2<FAST>(hz01 + vt01 - (f2){Rh.x, Rh.y}, denom, r_denom);
+    const f2 pu23 = fdiv2<FAST>(hz23 + vt23 - (f2){Rh.z, Rh.w}, denom, r_denom);
+    const float omega = 0.75f;
+    const float om1 = 1.0f - omega;
+    const f2 n01 = omega * pu01 + om1 * c01;
+    const f2 n23 = omega * pu23 + om1 * c23;
+    return make_float4(n01.x, n01.y, n23.x, n23.y);
 }
 
 // Exhaustive proof of the fast forms for one divisor c (r = RN(1/c)):
@@ -509,25 +547,10 @@ struct TbWave {
                                             const float4 &Rh) const {
         const float L0 = from_left(Cc.w);
         const float R3 = from_right(Cc.x);
-        const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
-        const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
-        const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
-        const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
-        const float bb[4] = {B.x, B.y, B.z, B.w};
-        const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
-        const float omega = 0.75f;
-        const float om1 = 1.0f - omega;
-        float n[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
-            const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
-            const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
-            n[k] = omega * p_update + om1 * cc[k];
-        }
-        float4 o = make_float4(n[0], n[1], n[2], n[3]);
+        float4 o = jacobi_row4<FAST>(B, Cc, Tp, Rh, L0, R3, dx_sq, dy_sq, denom, r_dx_sq,
+                                     r_dy_sq, r_denom);
         if (EDGE) {
-            if (ch == 0) o.x = n[1];
+            if (ch == 0) o.x = o.y;
             if (ch == nch - 1) o.w = 0.0f;
         }
         return o;
@@ -559,11 +582,21 @@ struct TbWave {
                 if (EDGE && r == g_first) W[s][(V + 2) % 3] = n; // P(i,0) = P(i,1)
             } else {
                 // final stage, rows r0 <= r < r1 (v >= 2T, v < S)
-                if (r < nyl && r >= 0 && out_lane) {
-                    if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                    if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                    if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                    if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                if (r < nyl && r >= 0) {
+                    if (EDGE) {
+                        if (out_lane) {
+                            if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                            if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                            if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                            if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                        }
+                    } else {
+                        // interior wave: every column of an output lane is a
+                        // residual column; halo lanes are cleared at the end
+                        m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
+                                        fabsf(n.z - C.z)),
+                                  fabsf(n.w - C.w));
+                    }
                 }
                 if (out_lane) {
                     *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
@@ -692,7 +725,8 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     w.RH[1] = w.ld4(w.rs_r, w.k_first);
 #pragma unroll
     for (int q = 2; q < 6; ++q) w.RH[q] = z4;
-    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 1);
+    // interior waves store chunks 1 .. nch-3 only (all residual columns)
+    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 2);
     const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;   // every row any stage touches
     auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
     const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
@@ -700,7 +734,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
         w.template run<true>();
     else
         w.template run<false>();
-    const float m = wave_max(w.m);
+    const float m = wave_max(w.out_lane ? w.m : 0.0f);
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
@@ -738,25 +772,10 @@ struct TbDeep {
                                             const float4 &Rh) const {
         const float L0 = from_left(Cc.w);
         const float R3 = from_right(Cc.x);
-        const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
-        const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
-        const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
-        const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
-        const float bb[4] = {B.x, B.y, B.z, B.w};
-        const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
-        const float omega = 0.75f;
-        const float om1 = 1.0f - omega;
-        float n[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
-            const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
-            const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
-            n[k] = omega * p_update + om1 * cc[k];
-        }
-        float4 o = make_float4(n[0], n[1], n[2], n[3]);
+        float4 o = jacobi_row4<FAST>(B, Cc, Tp, Rh, L0, R3, dx_sq, dy_sq, denom, r_dx_sq,
+                                     r_dy_sq, r_denom);
         if (EDGE) {
-            if (ch == 0) o.x = n[1];
+            if (ch == 0) o.x = o.y;
             if (ch == nch - 1) o.w = 0.0f;
         }
         return o;
@@ -785,11 +804,21 @@ struct TbDeep {
                 W[s][V % 3] = n;
                 if (EDGE && r == g_first) W[s][(V + 2) % 3] = n;
             } else {
-                if (r < nyl && r >= 0 && out_lane) {
-                    if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                    if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                    if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                    if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                if (r < nyl && r >= 0) {
+                    if (EDGE) {
+                        if (out_lane) {
+                            if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                            if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                            if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                            if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                        }
+                    } else {
+                        // interior wave: every column of an output lane is a
+                        // residual column; halo lanes are cleared at the end
+                        m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
+                                        fabsf(n.z - C.z)),
+                                  fabsf(n.w - C.w));
+                    }
                 }
                 if (out_lane) {
                     *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
@@ -889,7 +918,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
     }
     w.PF[0] = w.ld4(w.rs_p, w.k_first);
     w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
-    const bool col_edge = (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 1);
+    const bool col_edge = (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 2);
     const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;
     auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
     const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
@@ -897,7 +926,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
         w.template run<true>();
     else
         w.template run<false>();
-    const float m = wave_max(w.m);
+    const float m = wave_max(w.out_lane ? w.m : 0.0f);
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
@@ -936,25 +965,10 @@ struct TbSkew {
                                             const float4 &Rh) const {
         const float L0 = from_left(Cc.w);
         const float R3 = from_right(Cc.x);
-        const float cc[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
-        const float rr[4] = {Cc.y, Cc.z, Cc.w, R3};
-        const float ll[4] = {L0, Cc.x, Cc.y, Cc.z};
-        const float tt[4] = {Tp.x, Tp.y, Tp.z, Tp.w};
-        const float bb[4] = {B.x, B.y, B.z, B.w};
-        const float hh[4] = {Rh.x, Rh.y, Rh.z, Rh.w};
-        const float omega = 0.75f;
-        const float om1 = 1.0f - omega;
-        float n[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float horizontal = fdiv<FAST>(rr[k] + ll[k], dx_sq, r_dx_sq);
-            const float vertical = fdiv<FAST>(tt[k] + bb[k], dy_sq, r_dy_sq);
-            const float p_update = fdiv<FAST>(horizontal + vertical - hh[k], denom, r_denom);
-            n[k] = omega * p_update + om1 * cc[k];
-        }
-        float4 o = make_float4(n[0], n[1], n[2], n[3]);
+        float4 o = jacobi_row4<FAST>(B, Cc, Tp, Rh, L0, R3, dx_sq, dy_sq, denom, r_dx_sq,
+                                     r_dy_sq, r_denom);
         if (EDGE) {
-            if (ch == 0) o.x = n[1];
+            if (ch == 0) o.x = o.y;
             if (ch == nch - 1) o.w = 0.0f;
         }
         return o;
@@ -982,11 +996,21 @@ struct TbSkew {
                 if (EDGE && r == g_top) n = W[s][md(V - 2 * s - 1, 3)];   // = row ny-2
                 nw[s] = n;
             } else {
-                if (r < nyl && r >= 0 && out_lane) {
-                    if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                    if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                    if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                    if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                if (r < nyl && r >= 0) {
+                    if (EDGE) {
+                        if (out_lane) {
+                            if (e0) m = fmaxf(m, fabsf(n.x - C.x));
+                            if (e1) m = fmaxf(m, fabsf(n.y - C.y));
+                            if (e2) m = fmaxf(m, fabsf(n.z - C.z));
+                            if (e3) m = fmaxf(m, fabsf(n.w - C.w));
+                        }
+                    } else {
+                        // interior wave: every column of an output lane is a
+                        // residual column; halo lanes are cleared at the end
+                        m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
+                                        fabsf(n.z - C.z)),
+                                  fabsf(n.w - C.w));
+                    }
                 }
                 if (out_lane && (WARM || r < r1)) {
                     *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
@@ -1096,7 +1120,8 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb2(
     w.PF[2] = w.ld4(w.rs_p, w.k_first + 2);
     w.RH[0] = w.ld4(w.rs_r, w.k_first - 1);
     w.RH[1] = w.ld4(w.rs_r, w.k_first);
-    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 1);
+    // interior waves store chunks 1 .. nch-3 only (all residual columns)
+    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 2);
     const int lo_row = w.k_first - 1, hi_row = w.k_first + w.S + 1;
     auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
     const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
@@ -1104,7 +1129,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb2(
         w.template run<true>();
     else
         w.template run<false>();
-    const float m = wave_max(w.m);
+    const float m = wave_max(w.out_lane ? w.m : 0.0f);
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
