@@ -64,7 +64,8 @@ struct Geom {
     int32_t tb_rows;      // fixed output rows per wave segment (0: balanced by tb_bpc)
     int32_t tb_bpc;       // target k_jacobi_tb blocks per CU (balanced segmentation)
     int32_t n_cu;         // compute units of the device
-    int32_t tb_kind;      // 1: k_jacobi_tb (chained stages), 2: k_jacobi_tb2 (skewed stages)
+    int32_t tb_kind;      // 1: k_jacobi_tb (T <= 4), 3: k_jacobi_tb3 (prefetch pipeline, T <= 8)
+    int32_t xcd_remap;    // renumber blocks so each XCD gets contiguous tiles (xcd_block)
 };
 
 struct Fields {

@@ -33,6 +33,19 @@ __device__ __forceinline__ float wave_max(float m) {
     return m;
 }
 
+// XCD-aware block order.  The dispatcher deals workgroups to the 8 XCDs
+// round-robin (block b -> XCD b % 8), and each XCD has its own L2; renumber
+// so XCD x works on one contiguous range of tiles (rows), keeping the rows
+// neighbouring tiles share (stencil rows, segment overlaps) in one L2.  The
+// last G % 8 blocks keep their own index.
+__device__ __forceinline__ int xcd_block(const Geom &g) {
+    const int b = (int)blockIdx.x, G = (int)gridDim.x;
+    if (!g.xcd_remap) return b;
+    const int per = G >> 3;
+    if (b >= (per << 3)) return b;
+    return (b & 7) * per + (b >> 3);
+}
+
 // Lane shifts on the VALU (DPP wave_shr:1 / wave_shl:1, gfx9 family) instead
 // of the LDS crossbar: lane l receives lane l-1 (from_left) or l+1
 // (from_right); the wave's end lanes receive 0 (bound_ctrl: no register
@@ -170,8 +183,9 @@ __global__ __launch_bounds__(kBlock) void k_copy_star(Fields f, int pass) {
 template <int SCHEME>
 __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float dt_override,
                                                         int row_lo, int nbx) {
-    const int i = 1 + (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
-    const int lj = row_lo + (int)(blockIdx.x / nbx);
+    const int bid = xcd_block(g);
+    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + bid / nbx;
     const int nx = g.nx, ny = g.ny, W = nx + 1;
     if (i > nx) return;
     const int j = g.j0 + lj;
@@ -245,8 +259,9 @@ __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float 
 template <int SCHEME>
 __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float dt_override,
                                                         int row_lo, int nbx) {
-    const int i = 1 + (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
-    const int lj = row_lo + (int)(blockIdx.x / nbx);
+    const int bid = xcd_block(g);
+    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + bid / nbx;
     const int nx = g.nx, ny = g.ny, W = nx + 1;
     if (i > nx - 1) return;
     const int j = g.j0 + lj;
@@ -325,8 +340,9 @@ __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float 
 __global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pass,
                                                        float dt_override, int nbx) {
     if (pass_off(f.ctl, pass)) return;
-    const int i = (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
-    const int lj = (int)(blockIdx.x / nbx);
+    const int bid = xcd_block(g);
+    const int i = (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = bid / nbx;
     const int nx = g.nx, W = nx + 1;
     if (i >= nx) return;
     const float dt = dt_of(f.ctl, dt_override);
@@ -373,7 +389,8 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
 
     const int nx = g.nx, nch = nx >> 2, hg = g.hg, nyl = g.nyl;
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    const int bx = (int)blockIdx.x % nbx, seg = (int)blockIdx.x / nbx;
+    const int bid = xcd_block(g);
+    const int bx = bid % nbx, seg = bid / nbx;
     const int wcol = bx * kJacWavesPerBlock + wave;
     if (wcol * 64 >= nch) return;                         // wave-uniform
     const int ch = wcol * 64 + lane;
@@ -669,8 +686,9 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     // every row/slot condition below becomes a scalar branch
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     w.lane = (int)threadIdx.x & 63;
-    const int wc = (int)blockIdx.x % nwc;
-    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
+    const int bid = xcd_block(g);
+    const int wc = bid % nwc;
+    const int seg = (bid / nwc) * kJacWavesPerBlock + wave;
     // balanced segments: nseg row ranges differing by at most one row
     const int nrows = out_hi - out_lo;
     if (seg >= nseg) return;
@@ -738,19 +756,41 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
 }
 
-// Deep temporal blocking (T up to 8): the k_jacobi_tb register march with H
-// halo lanes on each side of the wave (edge values go stale one element per
-// sweep, so H = ceil(T/4) lanes; 64-2H lanes are stored) and the rhs rows
-// carried down the stages in a shift register (stage s at slot k uses rhs row
-// k-s, which stage s-1 used one slot earlier), so only the period-2 prefetch
-// and the period-3 windows index rings and the slot loop unrolls by 6.
-template <int T, int FAST>
-struct TbDeep {
+// Deep temporal blocking with a prefetch pipeline (kind 3, T up to 8): the
+// k_jacobi_tb register march with H = ceil(T/4) halo lanes on each side of
+// the wave (edge values go stale one element per sweep; 64-2H lanes are
+// stored) and every HBM load issued PD slots before its first use, so each
+// wave keeps 2·PD row loads in flight instead of waiting on them:
+//   PQ[v % PD]        p' input row k_first+v, loaded PD slots ahead
+//   W[s][v % 3]       newest row of stage s (stage 0 = input)
+//   RH[q % NR]        rhs row k_first+q; stage s at slot v reads q = v-s, the
+//                     load at slot v fetches q = v-1+PD (NR = T+PD rows live)
+// The slot loop is unrolled by U = lcm(3, PD, NR) so every ring index is a
+// compile-time constant.
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+constexpr int clcm(int a, int b) { return a / cgcd(a, b) * b; }
+
+// prefetch distance per T: deep enough to cover HBM latency, with a short
+// unroll period (U <= 24)
+template <int T> struct TbDepth { static constexpr int PD = 4; };
+template <> struct TbDepth<1> { static constexpr int PD = 2; };   // NR 3,  U 6
+template <> struct TbDepth<3> { static constexpr int PD = 3; };   // NR 6,  U 6
+template <> struct TbDepth<4> { static constexpr int PD = 2; };   // NR 6,  U 6
+template <> struct TbDepth<5> { static constexpr int PD = 3; };   // NR 8,  U 24
+template <> struct TbDepth<6> { static constexpr int PD = 3; };   // NR 9,  U 9
+template <> struct TbDepth<7> { static constexpr int PD = 2; };   // NR 9,  U 18
+// T 2: NR 6, U 12; T 8: NR 12, U 12
+
+template <int T, int FAST, int PD_ = TbDepth<T>::PD>
+struct TbPipe {
+    static constexpr int PD = PD_;
+    static constexpr int NR = T + PD;
+    static constexpr int U = clcm(clcm(3, PD), NR);
     static constexpr int H = (T + 3) / 4;
     static constexpr int OUTL = 64 - 2 * H;
     float4 W[T][3];
-    float4 RH[T];        // RH[s] = rhs row k-1-s at slot k (before the shift)
-    float4 PF[2];
+    float4 RH[NR];
+    float4 PQ[PD];
     int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
     int ch, col, lane, off0;
     bool out_lane, e0, e1, e2, e3;
@@ -781,28 +821,27 @@ struct TbDeep {
         return o;
     }
 
+    // Slot v (k = k_first + v).  V == v (mod U) fixes every ring index; in the
+    // warm-up (GUARD 0) V == v and stage s only runs from slot 2s on; GUARD 2
+    // is the final partial group (slots past the segment end return).
     template <int V, int GUARD, bool EDGE>
     __device__ __forceinline__ void slot(int v) {
         if (GUARD == 2 && v >= S) return;
         const int k = k_first + v;
-        W[0][V % 3] = PF[V % 2];
-        PF[V % 2] = ld4(rs_p, k + 2);
-        // rhs: stage s now needs row k-s, i.e. what stage s-1 had last slot
-#pragma unroll
-        for (int s = T - 1; s >= 1; --s) RH[s] = RH[s - 1];
-        RH[0] = ld4(rs_r, k - 1);
+        W[0][V % 3] = PQ[V % PD];                              // input row k
+        PQ[V % PD] = ld4(rs_p, k + PD);
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
-            if (GUARD == 0 && V < 2 * s) continue;
+            if (GUARD == 0 && V < 2 * s) continue;              // compile-time
             const int r = k - s;
-            const float4 &B = W[s - 1][(V + 1) % 3];
-            const float4 &C = W[s - 1][(V + 2) % 3];
-            const float4 &Tp = W[s - 1][V % 3];
-            float4 n = stage<EDGE>(B, C, Tp, RH[s - 1]);
+            const float4 &B = W[s - 1][(V + 1) % 3];            // stage s-1, row r-1
+            const float4 &C = W[s - 1][(V + 2) % 3];            //              row r
+            const float4 &Tp = W[s - 1][V % 3];                 //              row r+1
+            float4 n = stage<EDGE>(B, C, Tp, RH[(V - s + NR * 8) % NR]);
             if (s < T) {
-                if (EDGE && r == g_top) n = W[s][(V + 2) % 3];
+                if (EDGE && r == g_top) n = W[s][(V + 2) % 3];  // P(i,ny-1) = P(i,ny-2)
                 W[s][V % 3] = n;
-                if (EDGE && r == g_first) W[s][(V + 2) % 3] = n;
+                if (EDGE && r == g_first) W[s][(V + 2) % 3] = n;   // P(i,0) = P(i,1)
             } else {
                 if (r < nyl && r >= 0) {
                     if (EDGE) {
@@ -813,8 +852,6 @@ struct TbDeep {
                             if (e3) m = fmaxf(m, fabsf(n.w - C.w));
                         }
                     } else {
-                        // interior wave: every column of an output lane is a
-                        // residual column; halo lanes are cleared at the end
                         m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
                                         fabsf(n.z - C.z)),
                                   fabsf(n.w - C.w));
@@ -829,6 +866,7 @@ struct TbDeep {
                 }
             }
         }
+        RH[(V - 1 + PD + NR) % NR] = ld4(rs_r, k - 1 + PD);    // rhs row k-1+PD
     }
 
     template <int V, bool EDGE>
@@ -839,23 +877,21 @@ struct TbDeep {
         }
     }
 
-    template <int GUARD, bool EDGE>
+    template <int J, int GUARD, bool EDGE>
     __device__ __forceinline__ void group(int base) {
-        slot<2 * T + 0, GUARD, EDGE>(base + 0);
-        slot<2 * T + 1, GUARD, EDGE>(base + 1);
-        slot<2 * T + 2, GUARD, EDGE>(base + 2);
-        slot<2 * T + 3, GUARD, EDGE>(base + 3);
-        slot<2 * T + 4, GUARD, EDGE>(base + 4);
-        slot<2 * T + 5, GUARD, EDGE>(base + 5);
+        if constexpr (J < U) {
+            slot<2 * T + J, GUARD, EDGE>(base + J);
+            group<J + 1, GUARD, EDGE>(base);
+        }
     }
 
     template <bool EDGE>
     __device__ __forceinline__ void run() {
         warmup<0, EDGE>();
         int base = 2 * T;
-        const int full_end = 2 * T + ((S - 2 * T) / 6) * 6;
-        for (; base < full_end; base += 6) group<1, EDGE>(base);
-        if (base < S) group<2, EDGE>(base);
+        const int full_end = 2 * T + ((S - 2 * T) / U) * U;
+        for (; base < full_end; base += U) group<0, 1, EDGE>(base);
+        if (base < S) group<0, 2, EDGE>(base);
     }
 };
 
@@ -864,12 +900,13 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
     if (pass_off(ctl, pass)) return;
-    using Wv = TbDeep<T, FAST>;
+    using Wv = TbPipe<T, FAST>;
     Wv w;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     w.lane = (int)threadIdx.x & 63;
-    const int wc = (int)blockIdx.x % nwc;
-    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
+    const int bid = xcd_block(g);
+    const int wc = bid % nwc;
+    const int seg = (bid / nwc) * kJacWavesPerBlock + wave;
     const int nrows = out_hi - out_lo;
     if (seg >= nseg) return;
     w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
@@ -882,6 +919,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
     w.ch = wc * Wv::OUTL - Wv::H + w.lane;
     const bool in_dom = w.ch >= 0 && w.ch < w.nch;
     w.out_lane = in_dom && w.lane >= Wv::H && w.lane < 64 - Wv::H;
+    // buffers ping-pong once per LAUNCH: par = launches since the solve began
     const int si = (ctl->cur + par) & 1;
     float *src_alloc = si ? pb : pa;
     float *dst_alloc = si ? pa : pb;
@@ -912,217 +950,17 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
     w.S = (w.r1 - w.r0) + 2 * T;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int s = 0; s < T; ++s) {
-        w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
-        w.RH[s] = z4;
-    }
-    w.PF[0] = w.ld4(w.rs_p, w.k_first);
-    w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
-    const bool col_edge = (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 2);
-    const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;
-    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
-    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
-    if (col_edge || row_edge)
-        w.template run<true>();
-    else
-        w.template run<false>();
-    const float m = wave_max(w.out_lane ? w.m : 0.0f);
-    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
-}
-
-// Skewed variant of k_jacobi_tb: stage s computes row k - 2s at slot k, so it
-// reads only rows its predecessor finished in EARLIER slots; the T stages of a
-// slot are independent and the compiler can interleave them (instruction-level
-// parallelism of T per wave instead of a T-long dependency chain).  Rings:
-//   W[s][pos(row)], pos(row) = (row - k_first) % 3       (stage s < T window)
-//   PF[v % 3]   p' input row k_first+v, loaded three slots ahead
-//   RH[(q - k_first + 1) % 12]  rhs row q (rows k-2T .. k+1 live)
-// The slot loop is unrolled by 12 = lcm(3, 3, 12); stages are processed
-// T..1 within a slot (reads before the predecessor overwrites its oldest row).
-template <int T, int FAST>
-struct TbSkew {
-    float4 W[T][3];
-    float4 RH[12];
-    float4 PF[3];
-    int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
-    int ch, col, lane, off0;
-    bool out_lane, e0, e1, e2, e3;
-    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
-    __amdgpu_buffer_rsrc_t rs_p, rs_r;
-    float *dst;
-    float m;
-
-    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int row) const {
-        constexpr int kOOB = -16;
-        const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                           __uint_as_float(v.w));
-    }
-
-    template <bool EDGE>
-    __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
-                                            const float4 &Rh) const {
-        const float L0 = from_left(Cc.w);
-        const float R3 = from_right(Cc.x);
-        float4 o = jacobi_row4<FAST>(B, Cc, Tp, Rh, L0, R3, dx_sq, dy_sq, denom, r_dx_sq,
-                                     r_dy_sq, r_denom);
-        if (EDGE) {
-            if (ch == 0) o.x = o.y;
-            if (ch == nch - 1) o.w = 0.0f;
-        }
-        return o;
-    }
-
-    static constexpr int md(int a, int b) { return ((a % b) + b) % b; }
-
-    // slot v; V == v (mod 12) fixes ring indices; WARM: V == v exactly and
-    // stage s runs only from slot 3s; GUARD: slots past S return
-    template <int V, bool WARM, bool GUARD, bool EDGE>
-    __device__ __forceinline__ void slot(int v) {
-        if (GUARD && v >= S) return;
-        const int k = k_first + v;
-        float4 nw[T + 1];
-#pragma unroll
-        for (int s = T; s >= 1; --s) {
-            if (WARM && V < 3 * s) continue;                   // compile-time
-            const int r = k - 2 * s;
-            const float4 &B = W[s - 1][md(V - 2 * s - 1, 3)];   // stage s-1, row r-1
-            const float4 &C = W[s - 1][md(V - 2 * s, 3)];       //              row r
-            const float4 &Tp = W[s - 1][md(V - 2 * s + 1, 3)];  //              row r+1
-            const float4 &Rh = RH[md(V - 2 * s + 1, 12)];       // rhs row r
-            float4 n = stage<EDGE>(B, C, Tp, Rh);
-            if (s < T) {
-                if (EDGE && r == g_top) n = W[s][md(V - 2 * s - 1, 3)];   // = row ny-2
-                nw[s] = n;
-            } else {
-                if (r < nyl && r >= 0) {
-                    if (EDGE) {
-                        if (out_lane) {
-                            if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                            if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                            if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                            if (e3) m = fmaxf(m, fabsf(n.w - C.w));
-                        }
-                    } else {
-                        // interior wave: every column of an output lane is a
-                        // residual column; halo lanes are cleared at the end
-                        m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
-                                        fabsf(n.z - C.z)),
-                                  fabsf(n.w - C.w));
-                    }
-                }
-                if (out_lane && (WARM || r < r1)) {
-                    *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
-                    if (EDGE && r == g_first)
-                        *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
-                    if (EDGE && r == g_last)
-                        *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
-                }
-            }
-        }
-        // commit the new rows (after every stage of this slot read its inputs)
-#pragma unroll
-        for (int s = 1; s < T; ++s) {
-            if (WARM && V < 3 * s) continue;
-            W[s][md(V - 2 * s, 3)] = nw[s];
-            if (EDGE && (k - 2 * s) == g_first) W[s][md(V - 2 * s - 1, 3)] = nw[s];  // row 0
-        }
-        W[0][md(V, 3)] = PF[md(V, 3)];                          // input row k
-        PF[md(V, 3)] = ld4(rs_p, k + 3);
-        RH[md(V + 2, 12)] = ld4(rs_r, k + 1);
-    }
-
-    template <int V, bool EDGE>
-    __device__ __forceinline__ void warmup() {
-        if constexpr (V < 3 * T) {
-            slot<V, true, false, EDGE>(V);
-            warmup<V + 1, EDGE>();
-        }
-    }
-
-    template <int U, bool GUARD, bool EDGE>
-    __device__ __forceinline__ void group12(int base) {
-        if constexpr (U < 12) {
-            slot<3 * T + U, false, GUARD, EDGE>(base + U);
-            group12<U + 1, GUARD, EDGE>(base);
-        }
-    }
-
-    template <bool EDGE>
-    __device__ __forceinline__ void run() {
-        warmup<0, EDGE>();                               // slots 0 .. 3T-1
-        int base = 3 * T;
-        const int full_end = 3 * T + ((S - 3 * T) / 12) * 12;
-        for (; base < full_end; base += 12) group12<0, false, EDGE>(base);
-        if (base < S) group12<0, true, EDGE>(base);
-    }
-};
-
-template <int T, int FAST>
-__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb2(
-    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
-    if (pass_off(ctl, pass)) return;
-    TbSkew<T, FAST> w;
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    w.lane = (int)threadIdx.x & 63;
-    const int wc = (int)blockIdx.x % nwc;
-    const int seg = ((int)blockIdx.x / nwc) * kJacWavesPerBlock + wave;
-    // balanced segments: nseg row ranges differing by at most one row
-    const int nrows = out_hi - out_lo;
-    if (seg >= nseg) return;
-    w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
-    w.r1 = out_lo + (int)(((long)(seg + 1) * nrows) / nseg);
-    if (w.r0 >= w.r1) return;
-    w.nx = g.nx;
-    w.nch = g.nx >> 2;
-    w.hg = g.hg;
-    w.nyl = g.nyl;
-    w.ch = wc * 62 - 1 + w.lane;
-    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
-    w.out_lane = in_dom && w.lane >= 1 && w.lane <= 62;
-    const int si = (ctl->cur + par) & 1;
-    float *src_alloc = si ? pb : pa;
-    float *dst_alloc = si ? pa : pb;
-    const int pbytes = (w.nyl + 2 * w.hg) * w.nx * 4;
-    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
-    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)w.hg * w.nx), 0, pbytes,
-                                               0x00020000);
-    w.dst = dst_alloc + (long)w.hg * w.nx;
-    w.dx_sq = g.dx_sq;
-    w.dy_sq = g.dy_sq;
-    w.denom = g.denom;
-    w.r_dx_sq = g.r_dx_sq;
-    w.r_dy_sq = g.r_dy_sq;
-    w.r_denom = g.r_denom;
-    w.col = 4 * w.ch;
-    w.row_bytes = w.nx * 4;
-    w.off0 = in_dom ? (w.hg * w.nx + w.col) * 4 : -16;
-    w.e0 = (w.col >= 1) && (w.col <= w.nx - 8);
-    w.e1 = (w.col + 1 <= w.nx - 8);
-    w.e2 = (w.col + 2 <= w.nx - 8);
-    w.e3 = (w.col + 3 <= w.nx - 8);
-    w.g_first = 1 - g.j0;
-    w.g_last = g.ny - 2 - g.j0;
-    w.g_top = g.ny - 1 - g.j0;
-    w.g_zero = -g.j0;
-    w.m = 0.0f;
-    w.k_first = w.r0 - T;
-    w.S = (w.r1 - w.r0) + 3 * T;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
     for (int s = 0; s < T; ++s) w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
+    // prologue: p' rows k_first .. k_first+PD-1, rhs rows k_first .. k_first+PD-2
 #pragma unroll
-    for (int q = 0; q < 12; ++q) w.RH[q] = z4;
-    w.PF[0] = w.ld4(w.rs_p, w.k_first);
-    w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
-    w.PF[2] = w.ld4(w.rs_p, w.k_first + 2);
-    w.RH[0] = w.ld4(w.rs_r, w.k_first - 1);
-    w.RH[1] = w.ld4(w.rs_r, w.k_first);
+    for (int q = 0; q < Wv::PD; ++q) w.PQ[q] = w.ld4(w.rs_p, w.k_first + q);
+#pragma unroll
+    for (int q = 0; q < Wv::NR; ++q)
+        w.RH[q] = q < Wv::PD - 1 ? w.ld4(w.rs_r, w.k_first + q) : z4;
     // interior waves store chunks 1 .. nch-3 only (all residual columns)
-    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 2);
-    const int lo_row = w.k_first - 1, hi_row = w.k_first + w.S + 1;
+    const bool col_edge =
+        (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 2);
+    const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;   // every row any stage touches
     auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
     const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
     if (col_edge || row_edge)
@@ -1175,8 +1013,9 @@ __global__ __launch_bounds__(kBlock) void k_corrector(Geom g, Fields f, int pass
                                                       float dt_override, int nbx) {
     Ctl *c = f.ctl;
     if (pass_off(c, pass)) return;
-    const int i = (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
-    const int lj = (int)(blockIdx.x / nbx);                             // 0..nyl
+    const int bid = xcd_block(g);
+    const int i = (bid % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
+    const int lj = bid / nbx;                                // 0..nyl
     const int nx = g.nx, W = nx + 1;
     if (i > nx) return;
     const float dt = dt_of(c, dt_override);
@@ -1273,8 +1112,9 @@ __global__ __launch_bounds__(1024) void k_boundary(Geom g, Fields f) {
 __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, float dt_override,
                                                            int nbx) {
     Ctl *c = f.ctl;
-    const int i = (int)(blockIdx.x % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
-    const int lj = (int)(blockIdx.x / nbx);                             // 0..nyl
+    const int bid = xcd_block(g);
+    const int i = (bid % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
+    const int lj = bid / nbx;                                // 0..nyl
     const int nx = g.nx, W = nx + 1;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
     if (i <= nx) {
@@ -1475,7 +1315,7 @@ template <int T>
 static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par, int out_lo,
                       int out_hi, hipStream_t s) {
     const int nch = g.nx / 4;
-    const int outl = g.tb_kind == 3 ? 64 - 2 * ((T + 3) / 4) : 62;
+    const int outl = g.tb_kind == 3 ? TbPipe<T, 1>::OUTL : 62;
     const int nwc = cdiv(nch, outl);
     // Segments per column strip: either fixed rows per wave (CFD_TB_ROWS) or
     // enough balanced segments for ~tb_bpc blocks per CU, so the grid lands
@@ -1505,18 +1345,6 @@ static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par,
         return;
     }
     if constexpr (T <= 4) {
-    if (g.tb_kind == 2) {
-        if (g.fastdiv == 1)
-            hipLaunchKernelGGL((k_jacobi_tb2<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, nseg);
-        else if (g.fastdiv == 2)
-            hipLaunchKernelGGL((k_jacobi_tb2<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, nseg);
-        else
-            hipLaunchKernelGGL((k_jacobi_tb2<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, nseg);
-        return;
-    }
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb,
                            f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);

@@ -469,7 +469,7 @@ void apply_params(cfd_model *m, const cfd_params *p) {
 // check on the device (a few ms; cached per divisor value).  x * RN(1/c) is
 // exact e.g. for the power-of-two divisors of the 2^k cavity grids; the
 // FMA-corrected form covers most other divisors; anything else keeps IEEE
-// division.  CFD_FASTDIV=0 forces IEEE.
+// division.  CFD_FASTDIV=0 forces IEEE, CFD_FASTDIV=2 prefers the FMA-corrected form.
 std::mutex g_div_mu;
 std::vector<std::pair<uint32_t, int>> g_div_cache;   // divisor bits -> ok mask (bit0 m1, bit1 m2)
 
@@ -510,6 +510,7 @@ int choose_division(hipStream_t s, Geom &g) {
         return rc;
     const int all = m1 & m2 & m3;
     g.fastdiv = (all & 1) ? 1 : (all & 2) ? 2 : 0;
+    if (env && atoi(env) == 2 && (all & 2)) g.fastdiv = 2;   // test hook: prefer mode 2
     return 0;
 }
 
@@ -546,14 +547,22 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         if (rc0) return rc0;
     }
     g.tb_kind = 1;
-    if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = std::max(1, std::min(3, atoi(kv)));
+    if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = atoi(kv) >= 3 ? 3 : 1;
     m->t_max = g.tb_kind == 3 ? 8 : 4;
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
     m->t_max = std::min(m->t_max, g.tb_kind == 3 ? kMaxTemporal : 4);
-    g.tb_rows = 0;
+    // 24 output rows per wave segment: the best measured geometry at 4096^2
+    // (tools/tune_tb.py; segments whose slot count is a multiple of the
+    // 12-slot unrolled march avoid the remainder group)
+    g.tb_rows = 24;
     if (const char *rv = getenv("CFD_TB_ROWS")) g.tb_rows = std::max(4, std::min(1024, atoi(rv)));
     g.tb_bpc = 3;
-    if (const char *bv = getenv("CFD_TB_BPC")) g.tb_bpc = std::max(1, std::min(16, atoi(bv)));
+    if (const char *bv = getenv("CFD_TB_BPC")) {   // balanced segmentation instead
+        g.tb_bpc = std::max(1, std::min(16, atoi(bv)));
+        g.tb_rows = 0;
+    }
+    g.xcd_remap = 1;
+    if (const char *xv = getenv("CFD_XCD_REMAP")) g.xcd_remap = atoi(xv) ? 1 : 0;
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||

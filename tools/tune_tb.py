@@ -20,7 +20,9 @@ if os.environ.get("TUNE_CONFIGS"):
 grid = cfdamd.cavity_grid(n)
 params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
 models = {}
-for kind, t, r in configs:
+configs = [c if len(c) == 4 else tuple(c) + (1,) for c in configs]
+for kind, t, r, x in configs:
+    os.environ["CFD_XCD_REMAP"] = str(x)
     os.environ["CFD_TB_KIND"] = str(kind)
     os.environ["CFD_TEMPORAL"] = str(t)
     if r > 0:
@@ -32,7 +34,7 @@ for kind, t, r in configs:
     m = cfdamd.Model(grid, params)
     m.update_n(2)
     m.synchronize()
-    models[(kind, t, r)] = m
+    models[(kind, t, r, x)] = m
 res = {c: [] for c in configs}
 for rnd in range(3):
     for c in configs:
@@ -44,6 +46,6 @@ for rnd in range(3):
 out = []
 for c in configs:
     us = statistics.median(res[c])
-    out.append({"kind": c[0], "T": c[1], "R": c[2], "us_per_sweep": us,
+    out.append({"kind": c[0], "T": c[1], "R": c[2], "xcd": c[3], "us_per_sweep": us,
                 "cell_updates_per_s": n * n / (us * 1e-6)})
     print(json.dumps(out[-1]), flush=True)
