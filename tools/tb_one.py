@@ -1,5 +1,8 @@
-"""One model, one launch geometry (CFD_TB_KIND / CFD_TEMPORAL / CFD_TB_ROWS from
-the environment), a few bench steps: the unit rocprofv3 PMC passes attach to."""
+"""One model, one launch geometry (CFD_TB_KIND / CFD_TEMPORAL / CFD_TB_ROWS /
+CFD_XCD_REMAP from the environment) on the bench workload, in its own
+process: prints one JSON line with the solve time per sweep and the step time.
+Also the unit rocprofv3 PMC passes attach to.  Usage: tb_one.py [n] [steps]"""
+import json
 import os
 import sys
 
@@ -11,7 +14,12 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 m = cfdamd.Model(cfdamd.cavity_grid(n),
                  cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False))
-m.update_n(steps)
+m.update_n(2)
 m.synchronize()
-print(m.kernel_config, m.get_residuals().simulation_step)
+m.timing_begin()
+m.update_n(steps)
+tm = m.timing_end()
+print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("CFD_")},
+                  "kernel": m.kernel_config, "us_per_sweep": tm["solve_ms"] / tm["sweeps"] * 1e3,
+                  "ms_per_step": tm["step_ms"] / tm["steps"]}), flush=True)
 m.close()
