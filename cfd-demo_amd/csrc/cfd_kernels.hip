@@ -793,14 +793,18 @@ struct TbPipe {
     float4 PQ[PD];
     int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
     int ch, col, lane, off0;
+    int abase, dir;      // actual row = abase + dir * virtual row (dir -1: downward march)
     bool out_lane, e0, e1, e2, e3;
     float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
     __amdgpu_buffer_rsrc_t rs_p, rs_r;
     float *dst;
     float m;
 
-    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int row) const {
+    __device__ __forceinline__ int act(int row) const { return abase + dir * row; }
+
+    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int vrow) const {
         constexpr int kOOB = -16;
+        const int row = act(vrow);
         const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
         return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
@@ -843,7 +847,8 @@ struct TbPipe {
                 W[s][V % 3] = n;
                 if (EDGE && r == g_first) W[s][(V + 2) % 3] = n;   // P(i,0) = P(i,1)
             } else {
-                if (r < nyl && r >= 0) {
+                const int ra = act(r);
+                if (ra < nyl && ra >= 0) {
                     if (EDGE) {
                         if (out_lane) {
                             if (e0) m = fmaxf(m, fabsf(n.x - C.x));
@@ -858,7 +863,7 @@ struct TbPipe {
                     }
                 }
                 if (out_lane) {
-                    *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
+                    *reinterpret_cast<float4 *>(dst + (long)ra * nx + col) = n;
                     if (EDGE && r == g_first)
                         *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
                     if (EDGE && r == g_last)
@@ -948,22 +953,35 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
     w.m = 0.0f;
     w.k_first = w.r0 - T;
     w.S = (w.r1 - w.r0) + 2 * T;
+    w.abase = 0;
+    w.dir = 1;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int s = 0; s < T; ++s) w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
+    // interior waves store chunks 1 .. nch-3 only (all residual columns)
+    const bool col_edge =
+        (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 2);
+    // every row any stage touches, in either march direction (one spare each side)
+    const int lo_row = w.k_first - 2, hi_row = w.r1 + T + 2;
+    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
+    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
+    // Interior segments alternate their march direction (odd ones run
+    // downward through the mirrored row space — the stencil is symmetric, and
+    // f32 addition commutative, so the bits are the same): two neighbouring
+    // segments then read the rows they share at the same time, from L2,
+    // instead of one at its start and the other at its end.
+    const bool edge = col_edge || row_edge;
+    if (!edge && (seg & 1)) {
+        w.abase = w.r0 + w.r1 - 1;
+        w.dir = -1;
+    }
     // prologue: p' rows k_first .. k_first+PD-1, rhs rows k_first .. k_first+PD-2
 #pragma unroll
     for (int q = 0; q < Wv::PD; ++q) w.PQ[q] = w.ld4(w.rs_p, w.k_first + q);
 #pragma unroll
     for (int q = 0; q < Wv::NR; ++q)
         w.RH[q] = q < Wv::PD - 1 ? w.ld4(w.rs_r, w.k_first + q) : z4;
-    // interior waves store chunks 1 .. nch-3 only (all residual columns)
-    const bool col_edge =
-        (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 2);
-    const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;   // every row any stage touches
-    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
-    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
-    if (col_edge || row_edge)
+    if (edge)
         w.template run<true>();
     else
         w.template run<false>();
@@ -1112,70 +1130,84 @@ __global__ __launch_bounds__(1024) void k_boundary(Geom g, Fields f) {
 __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, float dt_override,
                                                            int nbx) {
     Ctl *c = f.ctl;
-    const int bid = xcd_block(g);
-    const int i = (bid % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
-    const int lj = bid / nbx;                                // 0..nyl
     const int nx = g.nx, W = nx + 1;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
-    if (i <= nx) {
-        const float dt = dt_of(c, dt_override);
-        const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
-        const int j = g.j0 + lj;
-        const long rp = (long)lj * nx;
-        if (lj < g.nyl) {
-            const long k = (long)lj * W + i;
-            float nw;
-            if (j == 0) {
-                nw = 0.0f;
-            } else if (j == g.ny - 1) {
-                nw = (g.bc_kind == 1 && i > 0 && i < nx) ? c->inlet : 0.0f;
-            } else if (i == 0) {
-                nw = g.bc_kind == 0 ? inlet_value(g, c->inlet, j) : 0.0f;
-            } else if (i == nx) {
-                // outflow copies the corrected face nx-1 (scalar tail association, Q9)
-                nw = g.bc_kind == 0
-                         ? f.u_star[k - 1] - dt * (pp[rp + nx - 1] - pp[rp + nx - 2]) / g.dx
-                         : 0.0f;
-            } else {
-                const float p_right = pp[rp + i];
-                const float p_left = pp[rp + i - 1];
-                nw = (i >= nx - 7) ? f.u_star[k] - dt * (p_right - p_left) / g.dx
-                                   : f.u_star[k] - dt * ((p_right - p_left) / g.dx);
+    // each block walks a contiguous run of (row, 256-column) tiles, so the
+    // residual maxima leave the block as 4 atomics, not 4 per wave per tile
+    const long ntiles = (long)nbx * (g.nyl + 1);
+    const int bid = xcd_block(g), G = (int)gridDim.x;
+    const long t_lo = ntiles * bid / G, t_hi = ntiles * (bid + 1) / G;
+    for (long t = t_lo; t < t_hi; ++t) {
+        const int i = (int)(t % nbx) * kBlock + (int)threadIdx.x;   // 0..nx
+        const int lj = (int)(t / nbx);                               // 0..nyl
+        if (i <= nx) {
+            const float dt = dt_of(c, dt_override);
+            const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+            const int j = g.j0 + lj;
+            const long rp = (long)lj * nx;
+            if (lj < g.nyl) {
+                const long k = (long)lj * W + i;
+                float nw;
+                if (j == 0) {
+                    nw = 0.0f;
+                } else if (j == g.ny - 1) {
+                    nw = (g.bc_kind == 1 && i > 0 && i < nx) ? c->inlet : 0.0f;
+                } else if (i == 0) {
+                    nw = g.bc_kind == 0 ? inlet_value(g, c->inlet, j) : 0.0f;
+                } else if (i == nx) {
+                    // outflow copies the corrected face nx-1 (scalar tail association, Q9)
+                    nw = g.bc_kind == 0
+                             ? f.u_star[k - 1] - dt * (pp[rp + nx - 1] - pp[rp + nx - 2]) / g.dx
+                             : 0.0f;
+                } else {
+                    const float p_right = pp[rp + i];
+                    const float p_left = pp[rp + i - 1];
+                    nw = (i >= nx - 7) ? f.u_star[k] - dt * (p_right - p_left) / g.dx
+                                       : f.u_star[k] - dt * ((p_right - p_left) / g.dx);
+                }
+                if (f.n_obs > 0 && (f.mask_u[k] & 2)) nw = 0.0f;
+                const float old = f.u[k];
+                f.u[k] = nw;
+                du = fmaxf(du, fabsf(nw - old));
+                mu = fmaxf(mu, fabsf(nw));
             }
-            if (f.n_obs > 0 && (f.mask_u[k] & 2)) nw = 0.0f;
-            const float old = f.u[k];
-            f.u[k] = nw;
-            du = fmaxf(0.f, fabsf(nw - old));
-            mu = fmaxf(0.f, fabsf(nw));
-        }
-        if (i < nx) {
-            const long k = rp + i;
-            float nw;
-            if (j == 0 || j == g.ny) {
-                nw = 0.0f;
-            } else {
-                const float p_top = pp[k];
-                const float p_bottom = pp[k - nx];
-                nw = f.v_star[k] - dt * ((p_top - p_bottom) / g.dy);
+            if (i < nx) {
+                const long k = rp + i;
+                float nw;
+                if (j == 0 || j == g.ny) {
+                    nw = 0.0f;
+                } else {
+                    const float p_top = pp[k];
+                    const float p_bottom = pp[k - nx];
+                    nw = f.v_star[k] - dt * ((p_top - p_bottom) / g.dy);
+                }
+                if (f.n_obs > 0 && (f.mask_v[k] & 2)) nw = 0.0f;
+                const float old = f.v[k];
+                f.v[k] = nw;
+                dv = fmaxf(dv, fabsf(nw - old));
+                mv = fmaxf(mv, fabsf(nw));
+                if (lj < g.nyl) f.p[k] = f.p[k] + pp[k];
             }
-            if (f.n_obs > 0 && (f.mask_v[k] & 2)) nw = 0.0f;
-            const float old = f.v[k];
-            f.v[k] = nw;
-            dv = fmaxf(0.f, fabsf(nw - old));
-            mv = fmaxf(0.f, fabsf(nw));
-            if (lj < g.nyl) f.p[k] = f.p[k] + pp[k];
         }
     }
+    __shared__ float red[kBlock / 64][4];
     du = wave_max(du);
     dv = wave_max(dv);
     mu = wave_max(mu);
     mv = wave_max(mv);
+    const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        uint32_t *r = c->red;
-        if (du > 0.f) atomicMax(&r[0], __float_as_uint(du));
-        if (dv > 0.f) atomicMax(&r[1], __float_as_uint(dv));
-        if (mu > 0.f) atomicMax(&r[2], __float_as_uint(mu));
-        if (mv > 0.f) atomicMax(&r[3], __float_as_uint(mv));
+        red[wv][0] = du;
+        red[wv][1] = dv;
+        red[wv][2] = mu;
+        red[wv][3] = mv;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float r = 0.f;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) r = fmaxf(r, red[w][threadIdx.x]);
+        if (r > 0.f) atomicMax(&c->red[threadIdx.x], __float_as_uint(r));
     }
 }
 
@@ -1396,8 +1428,9 @@ void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_overrid
 
 void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
     const int nbx = cdiv(g.nx + 1, kBlock);
-    hipLaunchKernelGGL(k_correct_finish, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f,
-                       dt_override, nbx);
+    const long ntiles = (long)nbx * (g.nyl + 1);
+    const int blocks = (int)std::min<long>(ntiles, 8L * g.n_cu);
+    hipLaunchKernelGGL(k_correct_finish, dim3(blocks), dim3(kBlock), 0, s, g, f, dt_override, nbx);
 }
 
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s) {

@@ -12,10 +12,17 @@ for c in "${LIST[@]}"; do
   IFS=',' read -r K T R <<< "$c"
   name="k${K}_t${T}_r${R}"
   echo "=== $name $(date +%T)"
-  CFD_TB_KIND=$K CFD_TEMPORAL=$T CFD_TB_ROWS=$R timeout -k 10 300 \
-    rocprofv3 --pmc $CTRS -d gpurun_out/pmc_$TAG -o $name --output-format csv \
-    -- python3 tools/tb_one.py 4096 2 > gpurun_out/pmc_$TAG/$name.log 2>&1
-  rc=$?
-  echo "rc=$rc"; tail -3 gpurun_out/pmc_$TAG/$name.log
-  if [ $rc -ge 124 ]; then exit $rc; fi
+  for pass in sq fetch write; do
+    case $pass in
+      sq) C="$CTRS";;
+      fetch) C="FETCH_SIZE";;
+      write) C="WRITE_SIZE";;
+    esac
+    CFD_TB_KIND=$K CFD_TEMPORAL=$T CFD_TB_ROWS=$R timeout -k 10 300 \
+      rocprofv3 --pmc $C -d gpurun_out/pmc_$TAG -o ${name}_$pass --output-format csv \
+      -- python3 tools/tb_one.py 4096 2 > gpurun_out/pmc_$TAG/${name}_$pass.log 2>&1
+    rc=$?
+    echo "rc=$rc"; tail -1 gpurun_out/pmc_$TAG/${name}_$pass.log
+    if [ $rc -ge 124 ]; then exit $rc; fi
+  done
 done
