@@ -1,0 +1,110 @@
+// cfd_device.h — device helpers shared by the kernel translation units
+// (cfd_kernels.hip, cfd_jacobi_tb1.hip, cfd_jacobi_pipe*.hip).  Everything is
+// internal to each translation unit (anonymous namespace).
+#pragma once
+#include "cfd_internal.h"
+
+#include <algorithm>
+
+namespace cfd {
+namespace {
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+
+constexpr int kBlock = 256;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float dt_of(const Ctl *c, float dt_override) {
+    return __builtin_isnan(dt_override) ? c->dt : dt_override;
+}
+
+__device__ __forceinline__ bool pass_off(const Ctl *c, int pass) {
+    return pass >= 0 && c->go[pass] == 0;
+}
+
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    return m;
+}
+
+// XCD-aware block order.  The dispatcher deals workgroups to the 8 XCDs
+// round-robin (block b -> XCD b % 8), and each XCD has its own L2; renumber
+// so XCD x works on one contiguous range of tiles (rows), keeping the rows
+// neighbouring tiles share (stencil rows, segment overlaps) in one L2.  The
+// last G % 8 blocks keep their own index.
+__device__ __forceinline__ int xcd_block(const Geom &g) {
+    const int b = (int)blockIdx.x, G = (int)gridDim.x;
+    if (!g.xcd_remap) return b;
+    const int per = G >> 3;
+    if (b >= (per << 3)) return b;
+    return (b & 7) * per + (b >> 3);
+}
+
+// Lane shifts on the VALU (DPP wave_shr:1 / wave_shl:1, gfx9 family) instead
+// of the LDS crossbar: lane l receives lane l-1 (from_left) or l+1
+// (from_right); the wave's end lanes receive 0 (bound_ctrl: no register
+// initialisation needed; they are halo lanes).
+__device__ __forceinline__ float from_left(float x) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float from_right(float x) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, true));
+}
+
+// x / c with the reference's IEEE rounding.  FAST 1 and 2 are used only for
+// divisors whose result equals IEEE `/` for every one of the 2^32 inputs,
+// proven on the device at model creation (verify_division, cfd_model.hip).
+template <int FAST>
+__device__ __forceinline__ float fdiv(float x, float c, float r) {
+    if (FAST == 1) return x * r;
+    if (FAST == 2) {
+        const float q0 = x * r;
+        const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
+        return __builtin_isfinite(q0) ? q : q0;
+    }
+    return x / c;
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int FAST>
+__device__ __forceinline__ f2 fdiv2(f2 x, float c, float r) {
+    if (FAST == 1) return x * r;                        // v_pk_mul_f32
+    return (f2){fdiv<FAST>(x.x, c, r), fdiv<FAST>(x.y, c, r)};
+}
+
+// One reference Jacobi update (model.rs:775-793) of the 4 consecutive
+// columns a lane holds, C = row j, B = row j-1, T = row j+1, Rh = rhs row j,
+// L0 / R3 = the columns left / right of the chunk.  The arithmetic is the
+// reference's, operation for operation, on column pairs: each pair is one
+// packed VOP3P instruction, and the horizontal sums are formed as
+// swap(C01) + (L0, C.z) and swap(C23) + (C.y, R3), so the swap folds into
+// op_sel and only two register moves remain per 4 columns (f32 addition is
+// commutative bit for bit).
+template <int FAST>
+__device__ __forceinline__ float4 jacobi_row4(const float4 &B, const float4 &C, const float4 &T,
+                                              const float4 &Rh, float L0, float R3, float dx_sq,
+                                              float dy_sq, float denom, float r_dx_sq,
+                                              float r_dy_sq, float r_denom) {
+    const f2 c01 = {C.x, C.y}, c23 = {C.z, C.w};
+    const f2 h01 = __builtin_shufflevector(c01, c01, 1, 0) + (f2){L0, C.z};
+    const f2 h23 = __builtin_shufflevector(c23, c23, 1, 0) + (f2){C.y, R3};
+    const f2 v01 = (f2){T.x, T.y} + (f2){B.x, B.y};
+    const f2 v23 = (f2){T.z, T.w} + (f2){B.z, B.w};
+    const f2 hz01 = fdiv2<FAST>(h01, dx_sq, r_dx_sq), hz23 = fdiv2<FAST>(h23, dx_sq, r_dx_sq);
+    const f2 vt01 = fdiv2<FAST>(v01, dy_sq, r_dy_sq), vt23 = fdiv2<FAST>(v23, dy_sq, r_dy_sq);
+    const f2 pu01 = fdiv2<FAST>(hz01 + vt01 - (f2){Rh.x, Rh.y}, denom, r_denom);
+    const f2 pu23 = fdiv2<FAST>(hz23 + vt23 - (f2){Rh.z, Rh.w}, denom, r_denom);
+    const float omega = 0.75f;
+    const float om1 = 1.0f - omega;
+    const f2 n01 = omega * pu01 + om1 * c01;
+    const f2 n23 = omega * pu23 + om1 * c23;
+    return make_float4(n01.x, n01.y, n23.x, n23.y);
+}
+
+}  // namespace
+}  // namespace cfd

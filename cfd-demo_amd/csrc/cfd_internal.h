@@ -64,7 +64,8 @@ struct Geom {
     int32_t tb_rows;      // fixed output rows per wave segment (0: balanced by tb_bpc)
     int32_t tb_bpc;       // target k_jacobi_tb blocks per CU (balanced segmentation)
     int32_t n_cu;         // compute units of the device
-    int32_t tb_kind;      // 1: k_jacobi_tb (T <= 4), 3: k_jacobi_tb3 (prefetch pipeline, T <= 8)
+    int32_t tb_kind;      // 1: k_jacobi_tb (T <= 4); prefetch pipeline (T <= 8) with
+                          // 3: 4 columns per lane, 4: 2 columns per lane
     int32_t xcd_remap;    // renumber blocks so each XCD gets contiguous tiles (xcd_block)
 };
 
@@ -98,6 +99,15 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
 // buffers flip once per launch).
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
                          int out_lo, int out_hi, hipStream_t s);
+// The block kernels behind it: k_jacobi_tb (T <= 4, cfd_jacobi_tb1.hip) and
+// the prefetch-pipelined march with 4 or 2 columns per lane (T <= 8,
+// cfd_jacobi_pipe4.hip / cfd_jacobi_pipe2.hip).
+void launch_tb1(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
+                int out_hi, hipStream_t s);
+void launch_pipe4(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
+                  int out_hi, hipStream_t s);
+void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
+                  int out_hi, hipStream_t s);
 // Exhaustive check over all 2^32 f32 inputs x of x/c against the two fast
 // forms; writes mismatch counts {mode1, mode2} to dev_counts (2 x u64).
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s);

@@ -8,108 +8,11 @@
 // f32 bit pattern of a non-negative value) are deterministic.
 //
 // Citations are /root/reference/src/model.rs line numbers.
-#include "cfd_internal.h"
-
-#include <algorithm>
+#include "cfd_device.h"
 
 namespace cfd {
 
 namespace {
-
-constexpr int kBlock = 256;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float dt_of(const Ctl *c, float dt_override) {
-    return __builtin_isnan(dt_override) ? c->dt : dt_override;
-}
-
-__device__ __forceinline__ bool pass_off(const Ctl *c, int pass) {
-    return pass >= 0 && c->go[pass] == 0;
-}
-
-__device__ __forceinline__ float wave_max(float m) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    return m;
-}
-
-// XCD-aware block order.  The dispatcher deals workgroups to the 8 XCDs
-// round-robin (block b -> XCD b % 8), and each XCD has its own L2; renumber
-// so XCD x works on one contiguous range of tiles (rows), keeping the rows
-// neighbouring tiles share (stencil rows, segment overlaps) in one L2.  The
-// last G % 8 blocks keep their own index.
-__device__ __forceinline__ int xcd_block(const Geom &g) {
-    const int b = (int)blockIdx.x, G = (int)gridDim.x;
-    if (!g.xcd_remap) return b;
-    const int per = G >> 3;
-    if (b >= (per << 3)) return b;
-    return (b & 7) * per + (b >> 3);
-}
-
-// Lane shifts on the VALU (DPP wave_shr:1 / wave_shl:1, gfx9 family) instead
-// of the LDS crossbar: lane l receives lane l-1 (from_left) or l+1
-// (from_right); the wave's end lanes receive 0 (bound_ctrl: no register
-// initialisation needed; they are halo lanes).
-__device__ __forceinline__ float from_left(float x) {
-    return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, true));
-}
-__device__ __forceinline__ float from_right(float x) {
-    return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, true));
-}
-
-// x / c with the reference's IEEE rounding.  FAST 1 and 2 are used only for
-// divisors whose result equals IEEE `/` for every one of the 2^32 inputs,
-// proven on the device at model creation (verify_division, cfd_model.hip).
-template <int FAST>
-__device__ __forceinline__ float fdiv(float x, float c, float r) {
-    if (FAST == 1) return x * r;
-    if (FAST == 2) {
-        const float q0 = x * r;
-        const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
-        return __builtin_isfinite(q0) ? q : q0;
-    }
-    return x / c;
-}
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-template <int FAST>
-__device__ __forceinline__ f2 fdiv2(f2 x, float c, float r) {
-    if (FAST == 1) return x * r;                        // v_pk_mul_f32
-    return (f2){fdiv<FAST>(x.x, c, r), fdiv<FAST>(x.y, c, r)};
-}
-
-// One reference Jacobi update (model.rs:775-793) of the 4 consecutive
-// columns a lane holds, C = row j, B = row j-1, T = row j+1, Rh = rhs row j,
-// L0 / R3 = the columns left / right of the chunk.  The arithmetic is the
-// reference's, operation for operation, on column pairs: each pair is one
-// packed VOP3P instruction, and the horizontal sums are formed as
-// swap(C01) + (L0, C.z) and swap(C23) + (C.y, R3), so the swap folds into
-// op_sel and only two register moves remain per 4 columns (f32 addition is
-// commutative bit for bit).
-template <int FAST>
-__device__ __forceinline__ float4 jacobi_row4(const float4 &B, const float4 &C, const float4 &T,
-                                              const float4 &Rh, float L0, float R3, float dx_sq,
-                                              float dy_sq, float denom, float r_dx_sq,
-                                              float r_dy_sq, float r_denom) {
-    const f2 c01 = {C.x, C.y}, c23 = {C.z, C.w};
-    const f2 h01 = __builtin_shufflevector(c01, c01, 1, 0) + (f2){L0, C.z};
-    const f2 h23 = __builtin_shufflevector(c23, c23, 1, 0) + (f2){C.y, R3};
-    const f2 v01 = (f2){T.x, T.y} + (f2){B.x, B.y};
-    const f2 v23 = (f2){T.z, T.w} + (f2){B.z, B.w};
-    const f2 hz01 = fdiv2<FAST>(h01, dx_sq, r_dx_sq), hz23 = fdiv2<FAST>(h23, dx_sq, r_dx_sq);
-    const f2 vt01 = fdiv2<FAST>(v01, dy_sq, r_dy_sq), vt23 = fdiv2<FAST>(v23, dy_sq, r_dy_sq);
-    const f2 pu01 = fdiv2<FAST>(hz01 + vt01 - (f2){Rh.x, Rh.y}, denom, r_denom);
-    const f2 pu23 = fdiv2<FAST>(hz23 + vt23 - (f2){Rh.z, Rh.w}, denom, r_denom);
-    const float omega = 0.75f;
-    const float om1 = 1.0f - omega;
-    const f2 n01 = omega * pu01 + om1 * c01;
-    const f2 n23 = omega * pu23 + om1 * c23;
-    return make_float4(n01.x, n01.y, n23.x, n23.y);
-}
-
 // Exhaustive proof of the fast forms for one divisor c (r = RN(1/c)):
 // counts inputs x where x*r (mode 1) or the corrected form (mode 2) differs
 // from IEEE x/c; NaN results compare equal to NaN.
@@ -512,483 +415,6 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it], __float_as_uint(m));
 }
 
-// T weighted-Jacobi sweeps in one launch (temporal blocking; fixed-count
-// solves only — the tolerance test needs every sweep's residual).
-//
-// A wave owns 64 float4 column chunks; lanes 0 and 63 are halo lanes whose
-// values go stale one element per sweep from the outside in, so for T <= 4
-// lanes 1..62 (248 columns) stay exact and are the only ones stored; wave
-// columns overlap by two chunks.  The wave marches a segment of R output rows
-// through T pipelined stages: at row slot k it loads input row k and stage s
-// (1..T) computes row k-s from stage s-1's window of rows k-s-1..k-s+1, so
-// every stage is one sweep of the reference, at R + 2T row slots per segment.
-// p' and rhs come from HBM once per launch (12 B per T cell-updates).
-//
-// Per stage the p' boundary conditions of model.rs:807-815 are applied to the
-// window itself: column 0 takes column 1, column nx-1 is 0, global row ny-1
-// copies row ny-2, and global row 0 is patched with row 1 as soon as row 1 is
-// computed (before the next stage reads it).  Only the final stage is stored,
-// with the same fused boundary stores as k_jacobi.
-// Per-wave state of k_jacobi_tb.  Register rings are indexed by the slot
-// number v (0-based within the segment) modulo their period, so with the slot
-// loop unrolled by 6 (= lcm of the periods 2, 3 and 6) every index is a
-// compile-time constant and no window ever moves between registers:
-//   PF[v % 2]        p' input row k_first+v, loaded two slots ahead
-//   W[s][v % 3]      newest row of stage s (stage 0 = input)
-//   RH[(q-k_first+1) % 6]  rhs row q (rows k-4 .. k+1 live at slot k)
-template <int T, int FAST>
-struct TbWave {
-    float4 W[T][3];
-    float4 RH[6];
-    float4 PF[2];
-    // geometry (wave-uniform scalars unless noted)
-    int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
-    int ch, col, lane, off0;    // per lane
-    bool out_lane, e0, e1, e2, e3;
-    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
-    __amdgpu_buffer_rsrc_t rs_p, rs_r;
-    float *dst;
-    float m;
-
-    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int row) const {
-        constexpr int kOOB = -16;
-        const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                           __uint_as_float(v.w));
-    }
-
-    // one reference sweep of one row (model.rs:775-793 + BCs :807-815 per column)
-    template <bool EDGE>
-    __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
-                                            const float4 &Rh) const {
-        const float L0 = from_left(Cc.w);
-        const float R3 = from_right(Cc.x);
-        float4 o = jacobi_row4<FAST>(B, Cc, Tp, Rh, L0, R3, dx_sq, dy_sq, denom, r_dx_sq,
-                                     r_dy_sq, r_denom);
-        if (EDGE) {
-            if (ch == 0) o.x = o.y;
-            if (ch == nch - 1) o.w = 0.0f;
-        }
-        return o;
-    }
-
-    // Slot v of the segment.  V is a compile-time value with V == v (mod 6)
-    // that fixes every ring index; in the warm-up (GUARD == 0, V == v
-    // exactly) it also decides at compile time which stages already have
-    // rows to compute (stage s starts at slot 2s).  GUARD == 2 is the final
-    // partial group: slots past the segment end return (uniform branch).
-    template <int V, int GUARD, bool EDGE>
-    __device__ __forceinline__ void slot(int v) {
-        if (GUARD == 2 && v >= S) return;
-        const int k = k_first + v;
-        W[0][V % 3] = PF[V % 2];                             // input row k
-        PF[V % 2] = ld4(rs_p, k + 2);                        // two slots ahead
-#pragma unroll
-        for (int s = 1; s <= T; ++s) {
-            if (GUARD == 0 && V < 2 * s) continue;            // compile-time
-            const int r = k - s;
-            const float4 &B = W[s - 1][(V + 1) % 3];          // stage s-1, row r-1
-            const float4 &C = W[s - 1][(V + 2) % 3];          //              row r
-            const float4 &Tp = W[s - 1][V % 3];               //              row r+1
-            const float4 &Rh = RH[(V - s + 1 + 6) % 6];       // rhs row r
-            float4 n = stage<EDGE>(B, C, Tp, Rh);
-            if (s < T) {
-                if (EDGE && r == g_top) n = W[s][(V + 2) % 3];   // P(i,ny-1) = P(i,ny-2)
-                W[s][V % 3] = n;
-                if (EDGE && r == g_first) W[s][(V + 2) % 3] = n; // P(i,0) = P(i,1)
-            } else {
-                // final stage, rows r0 <= r < r1 (v >= 2T, v < S)
-                if (r < nyl && r >= 0) {
-                    if (EDGE) {
-                        if (out_lane) {
-                            if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                            if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                            if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                            if (e3) m = fmaxf(m, fabsf(n.w - C.w));
-                        }
-                    } else {
-                        // interior wave: every column of an output lane is a
-                        // residual column; halo lanes are cleared at the end
-                        m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
-                                        fabsf(n.z - C.z)),
-                                  fabsf(n.w - C.w));
-                    }
-                }
-                if (out_lane) {
-                    *reinterpret_cast<float4 *>(dst + (long)r * nx + col) = n;
-                    if (EDGE && r == g_first)
-                        *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
-                    if (EDGE && r == g_last)
-                        *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
-                }
-            }
-        }
-        RH[(V + 2) % 6] = ld4(rs_r, k + 1);                   // rhs row k+1
-    }
-
-    template <int V, bool EDGE>
-    __device__ __forceinline__ void warmup() {
-        if constexpr (V < 2 * T) {
-            slot<V, 0, EDGE>(V);
-            warmup<V + 1, EDGE>();
-        }
-    }
-
-    // steady-state group of 6 slots starting at v = base (base == 2T mod 6)
-    template <int GUARD, bool EDGE>
-    __device__ __forceinline__ void group(int base) {
-        slot<2 * T + 0, GUARD, EDGE>(base + 0);
-        slot<2 * T + 1, GUARD, EDGE>(base + 1);
-        slot<2 * T + 2, GUARD, EDGE>(base + 2);
-        slot<2 * T + 3, GUARD, EDGE>(base + 3);
-        slot<2 * T + 4, GUARD, EDGE>(base + 4);
-        slot<2 * T + 5, GUARD, EDGE>(base + 5);
-    }
-
-    // the whole segment; EDGE = the wave touches a domain boundary (column 0
-    // or nx-1, or a global row 0/1/ny-2/ny-1 in any stage) and needs the
-    // boundary-condition logic; interior waves skip it entirely
-    template <bool EDGE>
-    __device__ __forceinline__ void run() {
-        warmup<0, EDGE>();                              // slots 0 .. 2T-1
-        int base = 2 * T;
-        const int full_end = 2 * T + ((S - 2 * T) / 6) * 6;
-        for (; base < full_end; base += 6) group<1, EDGE>(base);
-        if (base < S) group<2, EDGE>(base);             // final partial group
-    }
-};
-
-// T weighted-Jacobi sweeps in one launch (temporal blocking; fixed-count
-// solves only — the tolerance test needs every sweep's residual).
-//
-// A wave owns 64 float4 column chunks; lanes 0 and 63 are halo lanes whose
-// values go stale one element per sweep from the outside in, so for T <= 4
-// lanes 1..62 (248 columns) stay exact and are the only ones stored; wave
-// columns overlap by two chunks.  The wave marches a segment of R output rows
-// through T pipelined stages: at row slot k it loads input row k and stage s
-// (1..T) computes row k-s from stage s-1's window of rows k-s-1..k-s+1, so
-// every stage is one sweep of the reference, at R + 2T row slots per segment.
-// p' and rhs come from HBM once per launch (12 B per T cell-updates).
-//
-// Per stage the p' boundary conditions of model.rs:807-815 are applied to the
-// window itself: column 0 takes column 1, column nx-1 is 0, global row ny-1
-// copies row ny-2, and global row 0 is patched with row 1 as soon as row 1 is
-// computed (before the next stage reads it).  Only the final stage is stored,
-// with the same fused boundary stores as k_jacobi.
-template <int T, int FAST>
-__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
-    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
-    if (pass_off(ctl, pass)) return;
-    TbWave<T, FAST> w;
-    // the wave index is uniform; readfirstlane lets the compiler see it, so
-    // every row/slot condition below becomes a scalar branch
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    w.lane = (int)threadIdx.x & 63;
-    const int bid = xcd_block(g);
-    const int wc = bid % nwc;
-    const int seg = (bid / nwc) * kJacWavesPerBlock + wave;
-    // balanced segments: nseg row ranges differing by at most one row
-    const int nrows = out_hi - out_lo;
-    if (seg >= nseg) return;
-    w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
-    w.r1 = out_lo + (int)(((long)(seg + 1) * nrows) / nseg);
-    if (w.r0 >= w.r1) return;
-    w.nx = g.nx;
-    w.nch = g.nx >> 2;
-    w.hg = g.hg;
-    w.nyl = g.nyl;
-    w.ch = wc * 62 - 1 + w.lane;
-    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
-    w.out_lane = in_dom && w.lane >= 1 && w.lane <= 62;
-
-    // buffers ping-pong once per LAUNCH: par = launches since the solve began
-    const int si = (ctl->cur + par) & 1;
-    float *src_alloc = si ? pb : pa;
-    float *dst_alloc = si ? pa : pb;
-    const int pbytes = (w.nyl + 2 * w.hg) * w.nx * 4;
-    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
-    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)w.hg * w.nx), 0, pbytes,
-                                               0x00020000);
-    w.dst = dst_alloc + (long)w.hg * w.nx;
-    w.dx_sq = g.dx_sq;
-    w.dy_sq = g.dy_sq;
-    w.denom = g.denom;
-    w.r_dx_sq = g.r_dx_sq;
-    w.r_dy_sq = g.r_dy_sq;
-    w.r_denom = g.r_denom;
-    w.col = 4 * w.ch;
-    w.row_bytes = w.nx * 4;
-    w.off0 = in_dom ? (w.hg * w.nx + w.col) * 4 : -16;
-    w.e0 = (w.col >= 1) && (w.col <= w.nx - 8);
-    w.e1 = (w.col + 1 <= w.nx - 8);
-    w.e2 = (w.col + 2 <= w.nx - 8);
-    w.e3 = (w.col + 3 <= w.nx - 8);
-    w.g_first = 1 - g.j0;
-    w.g_last = g.ny - 2 - g.j0;
-    w.g_top = g.ny - 1 - g.j0;
-    w.g_zero = -g.j0;
-    w.m = 0.0f;
-    w.k_first = w.r0 - T;
-    w.S = (w.r1 - w.r0) + 2 * T;
-
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int s = 0; s < T; ++s) w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
-    // prologue loads: input rows k_first, k_first+1; rhs rows k_first-1, k_first
-    w.PF[0] = w.ld4(w.rs_p, w.k_first);
-    w.PF[1] = w.ld4(w.rs_p, w.k_first + 1);
-    w.RH[0] = w.ld4(w.rs_r, w.k_first - 1);
-    w.RH[1] = w.ld4(w.rs_r, w.k_first);
-#pragma unroll
-    for (int q = 2; q < 6; ++q) w.RH[q] = z4;
-    // interior waves store chunks 1 .. nch-3 only (all residual columns)
-    const bool col_edge = wc == 0 || (wc * 62 + 63 >= w.nch - 2);
-    const int lo_row = w.k_first - 1, hi_row = w.r1 + T + 1;   // every row any stage touches
-    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
-    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
-    if (col_edge || row_edge)
-        w.template run<true>();
-    else
-        w.template run<false>();
-    const float m = wave_max(w.out_lane ? w.m : 0.0f);
-    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
-}
-
-// Deep temporal blocking with a prefetch pipeline (kind 3, T up to 8): the
-// k_jacobi_tb register march with H = ceil(T/4) halo lanes on each side of
-// the wave (edge values go stale one element per sweep; 64-2H lanes are
-// stored) and every HBM load issued PD slots before its first use, so each
-// wave keeps 2·PD row loads in flight instead of waiting on them:
-//   PQ[v % PD]        p' input row k_first+v, loaded PD slots ahead
-//   W[s][v % 3]       newest row of stage s (stage 0 = input)
-//   RH[q % NR]        rhs row k_first+q; stage s at slot v reads q = v-s, the
-//                     load at slot v fetches q = v-1+PD (NR = T+PD rows live)
-// The slot loop is unrolled by U = lcm(3, PD, NR) so every ring index is a
-// compile-time constant.
-constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
-constexpr int clcm(int a, int b) { return a / cgcd(a, b) * b; }
-
-// prefetch distance per T: deep enough to cover HBM latency, with a short
-// unroll period (U <= 24)
-template <int T> struct TbDepth { static constexpr int PD = 4; };
-template <> struct TbDepth<1> { static constexpr int PD = 2; };   // NR 3,  U 6
-template <> struct TbDepth<3> { static constexpr int PD = 3; };   // NR 6,  U 6
-template <> struct TbDepth<4> { static constexpr int PD = 2; };   // NR 6,  U 6
-template <> struct TbDepth<5> { static constexpr int PD = 3; };   // NR 8,  U 24
-template <> struct TbDepth<6> { static constexpr int PD = 3; };   // NR 9,  U 9
-template <> struct TbDepth<7> { static constexpr int PD = 2; };   // NR 9,  U 18
-// T 2: NR 6, U 12; T 8: NR 12, U 12
-
-template <int T, int FAST, int PD_ = TbDepth<T>::PD>
-struct TbPipe {
-    static constexpr int PD = PD_;
-    static constexpr int NR = T + PD;
-    static constexpr int U = clcm(clcm(3, PD), NR);
-    static constexpr int H = (T + 3) / 4;
-    static constexpr int OUTL = 64 - 2 * H;
-    float4 W[T][3];
-    float4 RH[NR];
-    float4 PQ[PD];
-    int k_first, S, r0, r1, nyl, nch, nx, hg, g_first, g_last, g_top, g_zero, row_bytes;
-    int ch, col, lane, off0;
-    int abase, dir;      // actual row = abase + dir * virtual row (dir -1: downward march)
-    bool out_lane, e0, e1, e2, e3;
-    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
-    __amdgpu_buffer_rsrc_t rs_p, rs_r;
-    float *dst;
-    float m;
-
-    __device__ __forceinline__ int act(int row) const { return abase + dir * row; }
-
-    __device__ __forceinline__ float4 ld4(const __amdgpu_buffer_rsrc_t &rs, int vrow) const {
-        constexpr int kOOB = -16;
-        const int row = act(vrow);
-        const int o = (off0 < 0 || row < -hg || row >= nyl + hg) ? kOOB : off0 + row * row_bytes;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-        return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
-                           __uint_as_float(v.w));
-    }
-
-    template <bool EDGE>
-    __device__ __forceinline__ float4 stage(const float4 &B, const float4 &Cc, const float4 &Tp,
-                                            const float4 &Rh) const {
-        const float L0 = from_left(Cc.w);
-        const float R3 = from_right(Cc.x);
-        float4 o = jacobi_row4<FAST>(B, Cc, Tp, Rh, L0, R3, dx_sq, dy_sq, denom, r_dx_sq,
-                                     r_dy_sq, r_denom);
-        if (EDGE) {
-            if (ch == 0) o.x = o.y;
-            if (ch == nch - 1) o.w = 0.0f;
-        }
-        return o;
-    }
-
-    // Slot v (k = k_first + v).  V == v (mod U) fixes every ring index; in the
-    // warm-up (GUARD 0) V == v and stage s only runs from slot 2s on; GUARD 2
-    // is the final partial group (slots past the segment end return).
-    template <int V, int GUARD, bool EDGE>
-    __device__ __forceinline__ void slot(int v) {
-        if (GUARD == 2 && v >= S) return;
-        const int k = k_first + v;
-        W[0][V % 3] = PQ[V % PD];                              // input row k
-        PQ[V % PD] = ld4(rs_p, k + PD);
-#pragma unroll
-        for (int s = 1; s <= T; ++s) {
-            if (GUARD == 0 && V < 2 * s) continue;              // compile-time
-            const int r = k - s;
-            const float4 &B = W[s - 1][(V + 1) % 3];            // stage s-1, row r-1
-            const float4 &C = W[s - 1][(V + 2) % 3];            //              row r
-            const float4 &Tp = W[s - 1][V % 3];                 //              row r+1
-            float4 n = stage<EDGE>(B, C, Tp, RH[(V - s + NR * 8) % NR]);
-            if (s < T) {
-                if (EDGE && r == g_top) n = W[s][(V + 2) % 3];  // P(i,ny-1) = P(i,ny-2)
-                W[s][V % 3] = n;
-                if (EDGE && r == g_first) W[s][(V + 2) % 3] = n;   // P(i,0) = P(i,1)
-            } else {
-                const int ra = act(r);
-                if (ra < nyl && ra >= 0) {
-                    if (EDGE) {
-                        if (out_lane) {
-                            if (e0) m = fmaxf(m, fabsf(n.x - C.x));
-                            if (e1) m = fmaxf(m, fabsf(n.y - C.y));
-                            if (e2) m = fmaxf(m, fabsf(n.z - C.z));
-                            if (e3) m = fmaxf(m, fabsf(n.w - C.w));
-                        }
-                    } else {
-                        m = fmaxf(fmaxf(fmaxf(fmaxf(m, fabsf(n.x - C.x)), fabsf(n.y - C.y)),
-                                        fabsf(n.z - C.z)),
-                                  fabsf(n.w - C.w));
-                    }
-                }
-                if (out_lane) {
-                    *reinterpret_cast<float4 *>(dst + (long)ra * nx + col) = n;
-                    if (EDGE && r == g_first)
-                        *reinterpret_cast<float4 *>(dst + (long)g_zero * nx + col) = n;
-                    if (EDGE && r == g_last)
-                        *reinterpret_cast<float4 *>(dst + (long)g_top * nx + col) = n;
-                }
-            }
-        }
-        RH[(V - 1 + PD + NR) % NR] = ld4(rs_r, k - 1 + PD);    // rhs row k-1+PD
-    }
-
-    template <int V, bool EDGE>
-    __device__ __forceinline__ void warmup() {
-        if constexpr (V < 2 * T) {
-            slot<V, 0, EDGE>(V);
-            warmup<V + 1, EDGE>();
-        }
-    }
-
-    template <int J, int GUARD, bool EDGE>
-    __device__ __forceinline__ void group(int base) {
-        if constexpr (J < U) {
-            slot<2 * T + J, GUARD, EDGE>(base + J);
-            group<J + 1, GUARD, EDGE>(base);
-        }
-    }
-
-    template <bool EDGE>
-    __device__ __forceinline__ void run() {
-        warmup<0, EDGE>();
-        int base = 2 * T;
-        const int full_end = 2 * T + ((S - 2 * T) / U) * U;
-        for (; base < full_end; base += U) group<0, 1, EDGE>(base);
-        if (base < S) group<0, 2, EDGE>(base);
-    }
-};
-
-template <int T, int FAST>
-__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb3(
-    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
-    if (pass_off(ctl, pass)) return;
-    using Wv = TbPipe<T, FAST>;
-    Wv w;
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    w.lane = (int)threadIdx.x & 63;
-    const int bid = xcd_block(g);
-    const int wc = bid % nwc;
-    const int seg = (bid / nwc) * kJacWavesPerBlock + wave;
-    const int nrows = out_hi - out_lo;
-    if (seg >= nseg) return;
-    w.r0 = out_lo + (int)(((long)seg * nrows) / nseg);
-    w.r1 = out_lo + (int)(((long)(seg + 1) * nrows) / nseg);
-    if (w.r0 >= w.r1) return;
-    w.nx = g.nx;
-    w.nch = g.nx >> 2;
-    w.hg = g.hg;
-    w.nyl = g.nyl;
-    w.ch = wc * Wv::OUTL - Wv::H + w.lane;
-    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
-    w.out_lane = in_dom && w.lane >= Wv::H && w.lane < 64 - Wv::H;
-    // buffers ping-pong once per LAUNCH: par = launches since the solve began
-    const int si = (ctl->cur + par) & 1;
-    float *src_alloc = si ? pb : pa;
-    float *dst_alloc = si ? pa : pb;
-    const int pbytes = (w.nyl + 2 * w.hg) * w.nx * 4;
-    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
-    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)w.hg * w.nx), 0, pbytes,
-                                               0x00020000);
-    w.dst = dst_alloc + (long)w.hg * w.nx;
-    w.dx_sq = g.dx_sq;
-    w.dy_sq = g.dy_sq;
-    w.denom = g.denom;
-    w.r_dx_sq = g.r_dx_sq;
-    w.r_dy_sq = g.r_dy_sq;
-    w.r_denom = g.r_denom;
-    w.col = 4 * w.ch;
-    w.row_bytes = w.nx * 4;
-    w.off0 = in_dom ? (w.hg * w.nx + w.col) * 4 : -16;
-    w.e0 = (w.col >= 1) && (w.col <= w.nx - 8);
-    w.e1 = (w.col + 1 <= w.nx - 8);
-    w.e2 = (w.col + 2 <= w.nx - 8);
-    w.e3 = (w.col + 3 <= w.nx - 8);
-    w.g_first = 1 - g.j0;
-    w.g_last = g.ny - 2 - g.j0;
-    w.g_top = g.ny - 1 - g.j0;
-    w.g_zero = -g.j0;
-    w.m = 0.0f;
-    w.k_first = w.r0 - T;
-    w.S = (w.r1 - w.r0) + 2 * T;
-    w.abase = 0;
-    w.dir = 1;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int s = 0; s < T; ++s) w.W[s][0] = w.W[s][1] = w.W[s][2] = z4;
-    // interior waves store chunks 1 .. nch-3 only (all residual columns)
-    const bool col_edge =
-        (wc * Wv::OUTL - Wv::H <= 0) || (wc * Wv::OUTL - Wv::H + 63 >= w.nch - 2);
-    // every row any stage touches, in either march direction (one spare each side)
-    const int lo_row = w.k_first - 2, hi_row = w.r1 + T + 2;
-    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
-    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
-    // Interior segments alternate their march direction (odd ones run
-    // downward through the mirrored row space — the stencil is symmetric, and
-    // f32 addition commutative, so the bits are the same): two neighbouring
-    // segments then read the rows they share at the same time, from L2,
-    // instead of one at its start and the other at its end.
-    const bool edge = col_edge || row_edge;
-    if (!edge && (seg & 1)) {
-        w.abase = w.r0 + w.r1 - 1;
-        w.dir = -1;
-    }
-    // prologue: p' rows k_first .. k_first+PD-1, rhs rows k_first .. k_first+PD-2
-#pragma unroll
-    for (int q = 0; q < Wv::PD; ++q) w.PQ[q] = w.ld4(w.rs_p, w.k_first + q);
-#pragma unroll
-    for (int q = 0; q < Wv::NR; ++q)
-        w.RH[q] = q < Wv::PD - 1 ? w.ld4(w.rs_r, w.k_first + q) : z4;
-    if (edge)
-        w.template run<true>();
-    else
-        w.template run<false>();
-    const float m = wave_max(w.out_lane ? w.m : 0.0f);
-    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
-}
-
 // End of a pressure solve: how many sweeps ran, which buffer is current, the
 // returned residual (model.rs:816-823), and whether the corrector loop goes on
 // (model.rs:721-723).  Resets the per-sweep slots for the next solve.
@@ -1266,7 +692,6 @@ __global__ void k_step_finalize(Geom g, Fields f) {
     c->red[0] = c->red[1] = c->red[2] = c->red[3] = 0u;
 }
 
-inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 inline int copy_grid(size_t n4) {
     long b = cdiv((long)n4, kBlock);
@@ -1343,70 +768,15 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
                            f.ctl, pass, it, row_lo, row_hi, nbx);
 }
 
-template <int T>
-static void launch_tb(const Geom &g, const Fields &f, int pass, int it, int par, int out_lo,
-                      int out_hi, hipStream_t s) {
-    const int nch = g.nx / 4;
-    const int outl = g.tb_kind == 3 ? TbPipe<T, 1>::OUTL : 62;
-    const int nwc = cdiv(nch, outl);
-    // Segments per column strip: either fixed rows per wave (CFD_TB_ROWS) or
-    // enough balanced segments for ~tb_bpc blocks per CU, so the grid lands
-    // evenly on the CUs (an uneven block count left CUs idle: 544 blocks on
-    // 256 CUs ran at 71 % balance, 765 at ~100 %).
-    int nseg;
-    if (g.tb_rows > 0) {
-        nseg = cdiv(out_hi - out_lo, g.tb_rows);
-    } else {
-        const int blocks_per_strip = cdiv((long)g.tb_bpc * g.n_cu, nwc);
-        nseg = blocks_per_strip * kJacWavesPerBlock;
-        const int max_seg = (out_hi - out_lo) / 8;     // keep >= 8 rows per segment
-        if (nseg > max_seg) nseg = std::max(1, max_seg);
-    }
-    const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
-    float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
-    if (g.tb_kind == 3) {
-        if (g.fastdiv == 1)
-            hipLaunchKernelGGL((k_jacobi_tb3<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, nseg);
-        else if (g.fastdiv == 2)
-            hipLaunchKernelGGL((k_jacobi_tb3<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, nseg);
-        else
-            hipLaunchKernelGGL((k_jacobi_tb3<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                               pass, it, par, out_lo, out_hi, nwc, nseg);
-        return;
-    }
-    if constexpr (T <= 4) {
-    if (g.fastdiv == 1)
-        hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
-    else if (g.fastdiv == 2)
-        hipLaunchKernelGGL((k_jacobi_tb<T, 2>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
-    else
-        hipLaunchKernelGGL((k_jacobi_tb<T, 0>), grid, block, 0, s, g, pa, pb,
-                           f.rhs, f.ctl, pass, it, par, out_lo, out_hi, nwc, nseg);
-    }
-}
-
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
                          int out_lo, int out_hi, hipStream_t s) {
     if (out_hi <= out_lo) return;
-    if (T > 4 && g.tb_kind == 3) {
-        switch (T) {
-        case 5: launch_tb<5>(g, f, pass, it, par, out_lo, out_hi, s); break;
-        case 6: launch_tb<6>(g, f, pass, it, par, out_lo, out_hi, s); break;
-        case 7: launch_tb<7>(g, f, pass, it, par, out_lo, out_hi, s); break;
-        default: launch_tb<8>(g, f, pass, it, par, out_lo, out_hi, s); break;
-        }
-        return;
-    }
-    switch (T) {
-    case 1: launch_tb<1>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 2: launch_tb<2>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 3: launch_tb<3>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    default: launch_tb<4>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    }
+    if (g.tb_kind == 3)
+        launch_pipe4(g, f, T, pass, it, par, out_lo, out_hi, s);
+    else if (g.tb_kind == 4)
+        launch_pipe2(g, f, T, pass, it, par, out_lo, out_hi, s);
+    else
+        launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, s);
 }
 
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s) {

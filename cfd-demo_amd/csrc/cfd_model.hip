@@ -531,6 +531,9 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     g.j0 = (int)m->j0;
     g.nyl = (int)(m->j1 - m->j0);
     g.hg = hg;
+    // the kernels address a field slab with 32-bit byte offsets
+    if ((uint64_t)(g.nyl + 2 * hg + 2 * kGhostUV + 1) * (uint64_t)(nx + 1) * 4u >= (1ull << 31))
+        return fail(CFD_EINVAL, "slab too large for 32-bit buffer offsets (2 GiB per field)");
     g.dx = grid->lx / (float)grid->nx;   // src/app.rs:37
     g.dy = grid->ly / (float)grid->ny;   // src/app.rs:38
     g.ly = grid->ly;
@@ -547,10 +550,16 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         if (rc0) return rc0;
     }
     g.tb_kind = 1;
-    if (const char *kv = getenv("CFD_TB_KIND")) g.tb_kind = atoi(kv) >= 3 ? 3 : 1;
-    m->t_max = g.tb_kind == 3 ? 8 : 4;
+    if (const char *kv = getenv("CFD_TB_KIND")) {
+        const int k = atoi(kv);
+        g.tb_kind = (k == 3 || k == 4) ? k : 1;
+    }
+    // the pipelined kernels park masked lanes at a far voffset that must not
+    // wrap past 2^32 when the row offset is added: slabs up to 1 GiB per field
+    if ((uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u > (1ull << 30)) g.tb_kind = 1;
+    m->t_max = g.tb_kind == 1 ? 4 : 6;
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
-    m->t_max = std::min(m->t_max, g.tb_kind == 3 ? kMaxTemporal : 4);
+    m->t_max = std::min(m->t_max, g.tb_kind == 1 ? 4 : kMaxTemporal);
     // 24 output rows per wave segment: the best measured geometry at 4096^2
     // (tools/tune_tb.py; segments whose slot count is a multiple of the
     // 12-slot unrolled march avoid the remainder group)

@@ -265,10 +265,12 @@ def test_control_handle_run_loop():
     ("0", "1", "1"), ("0", "4", "1"), ("1", "1", "1"), ("1", "3", "1"), ("1", "4", "1"),
     ("1", "8", "3"), ("0", "8", "3"), ("1", "5", "3"), ("1", "6", "3"), ("1", "7", "3"),
     ("1", "4", "3"), ("1", "3", "3"), ("1", "2", "3"), ("1", "1", "3"), ("2", "8", "3"),
-    ("2", "4", "1")])
+    ("2", "4", "1"), ("1", "6", "4"), ("1", "8", "4"), ("0", "8", "4"), ("1", "4", "4"),
+    ("1", "7", "4"), ("1", "5", "4"), ("1", "3", "4"), ("1", "2", "4"), ("1", "1", "4"),
+    ("2", "6", "4")])
 def test_kernel_variants_bitwise(monkeypatch, fastdiv, temporal, kind):
-    """Every Jacobi kernel variant (IEEE or proven-exact fast division; 1..4
-    sweeps per launch) gives the oracle's bits, on a power-of-two cavity (where
+    """Every Jacobi kernel variant (IEEE or proven-exact fast division; 1..8
+    sweeps per launch; kinds 1, 3 and 4) gives the oracle's bits, on a power-of-two cavity (where
     the reciprocal multiply is exact) and on the reference's default channel
     grid (non-power-of-two divisors)."""
     c = _cfd()
