@@ -51,14 +51,21 @@ def cpu_info():
     return model, os.cpu_count()
 
 
-def cpu_baseline(nx, ny, iters, re, budget_s):
+def cpu_baseline(nx, ny, iters, re, budget_s, state):
     """The oracle (scalar/auto-vectorised C restatement, 1 thread, like the
-    reference's single worker thread model.rs:1287) on the same workload."""
+    reference's single worker thread model.rs:1287) on the same workload,
+    started from the GPU model's final state (so it sweeps the same developed,
+    mostly non-zero fields, subnormals included, as the reference would)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import OracleModel
     m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
                     jacobi_iters=iters, corrector_passes=0, tol_enabled=0)
-    m.update()   # step 0 (untimed warm-up: touches every page)
+    for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
+        m.field(k)[:] = state[k]
+    sc = m.scalars()
+    sc.step, sc.time, sc.dt = state["simulation_step"], state["simulation_time"], state["dt"]
+    m.set_scalars(sc)
+    m.update()   # untimed warm-up step: touches every page
     steps, t0 = 0, time.perf_counter()
     while True:
         m.update()
@@ -70,20 +77,43 @@ def cpu_baseline(nx, ny, iters, re, budget_s):
     return {"value": nx * ny * iters * steps / el, "unit": "cell-updates/s", "cores": 1,
             "kind": "port",
             "sample": f"{steps} full update() step(s) of the same {nx}x{ny} cavity "
-                      f"({iters} sweeps/step) after 1 warm-up step, oracle/cfd_oracle.c, "
+                      f"({iters} sweeps/step) from the GPU run's final state (step "
+                      f"{state['simulation_step']}) after 1 warm-up step, oracle/cfd_oracle.c, "
                       f"1 thread; ms/step {1e3 * el / steps:.0f}; host {model}, {ncpu} cpus"}
+
+
+def pmc_traffic(kernel, slab):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*/pmc_traffic.json, tools/pmc_traffic.py: 2 x FETCH_SIZE +
+    WRITE_SIZE per the gfx950 correction) measured on this slab shape."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic*.json")),
+                       reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and d.get("workload") == slab:
+            return k["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 400 steps from rest: the fields are developed (97 % of p' non-zero, vs
+    # 4 % at step 20), so the timed steps sweep representative data
+    ap.add_argument("--warmup", type=int, default=400)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--clock-warmup", type=float, default=0.0,
+                    help="seconds of steps on a scratch model before the measured one is "
+                         "created, so the GPU clocks have left their idle state")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -114,6 +144,14 @@ def main():
         obj = [cfdamd.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
+    if args.clock_warmup > 0 and world == 1:
+        scratch = cfdamd.Model(grid, params, device=local)
+        t_end = time.perf_counter() + args.clock_warmup
+        while time.perf_counter() < t_end:
+            scratch.update_n(4)
+            scratch.synchronize()
+        scratch.close()
+        del scratch
     model = cfdamd.Model(grid, params, device=local, n_ranks=n, rank=rank, unique_id=uid)
 
     def barrier():
@@ -141,16 +179,20 @@ def main():
     snap = model.get_snapshot()
     import numpy as np
     finite = bool(np.isfinite(snap.u).all() and np.isfinite(snap.v).all())
+    state = model.get_state()   # this rank's slab
+    nonzero = float(np.count_nonzero(state["p_prime"])) / max(state["p_prime"].size, 1)
 
     cells_local = nx * model.nyl
     kcfg = model.kernel_config
+    kern = model.jacobi_kernel
     T = kcfg["temporal"]
-    launches = max(args.steps * -(-args.iters // T), 1)   # ceil(iters / T) launches per solve
+    launches = max(args.steps * model.launches_per_solve(), 1)
     launch_ms = tm["solve_ms"] / launches
     # algorithmic bytes per launch = 12 B/cell-update x cells x sweeps per launch
     bytes_launch = BYTES_PER_CELL_UPDATE * cells_local * T
     achieved = bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
 
+    traffic, traffic_src = pmc_traffic(kern["name"], f"{nx}x{model.nyl}")
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -164,21 +206,23 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (lid-driven cavity from rest, build-defined BCs; SURVEY.md §8(d))",
+            "data": f"synthetic (lid-driven cavity from rest, build-defined BCs, SURVEY.md §8(d); "
+                    f"timed steps {args.warmup}..{args.warmup + args.steps} on the developed "
+                    f"fields, {100 * nonzero:.0f}% of p' non-zero)",
             "config": {
                 "workload": f"{nx}x{ny} lid-driven cavity Re={args.re:g}, {args.iters} Jacobi "
                             "sweeps/step, tolerance off, 0 extra corrector passes",
                 "grid": [nx, ny], "slab_per_gpu": [nx, model.nyl], "jacobi_iters": args.iters,
                 "parallelism": f"row-slab x{n}" + (f", halo depth {model.halo_depth}" if n > 1 else ""),
-                "kernel": (f"k_jacobi_tb<{T}> ({T} sweeps/launch, register-march temporal "
-                           "blocking)" if T > 1 else "k_jacobi (1 sweep/launch)"),
+                "kernel": f"{kern['name']} ({T} sweep(s)/launch, kind {kern['kind']})",
                 "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
                              "FMA-corrected (proven exact, 2^32 inputs)"][kcfg["fastdiv"]],
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "k_jacobi_tb" if T > 1 else "k_jacobi", "sweeps_per_launch": T,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_source": traffic_src,
+                "kernel": kern["name"], "sweeps_per_launch": T,
                 "avg_launch_us": launch_ms * 1e3,
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "timing": "HIP events on the model stream around each step's launch sequence, "
@@ -191,7 +235,7 @@ def main():
             "final_step": res.simulation_step, "final_dt": res.dt, "fields_finite": finite,
         }
         if n == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(nx, ny, args.iters, args.re, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(nx, ny, args.iters, args.re, args.cpu_budget, state)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

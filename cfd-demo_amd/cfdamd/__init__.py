@@ -328,6 +328,30 @@ class Model:
               load().cfd_get_kernel_config(self._h, C.byref(fd), C.byref(tb)))
         return {"fastdiv": fd.value, "temporal": tb.value}
 
+    def launches_per_solve(self) -> int:
+        """Jacobi launches of one fixed-count solve, from the same host plan
+        (cfd_plan_block) the runtime follows."""
+        tmax = self.kernel_config["temporal"]
+        iters = self.params.jacobi_iters
+        hg = self.halo_depth if self.n_ranks > 1 else 0
+        T, lo, hi, ex = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        it = n = 0
+        while it < iters:
+            check("cfd_plan_block", load().cfd_plan_block(
+                self.j0, self.nyl, self.grid.ny, hg, it, tmax, iters, C.byref(T), C.byref(lo),
+                C.byref(hi), C.byref(ex)))
+            it += T.value
+            n += 1
+        return n
+
+    @property
+    def jacobi_kernel(self) -> dict:
+        """Kind and rocprofv3 name of the kernel a fixed-count solve launches."""
+        kind, name = C.c_int(), C.create_string_buffer(96)
+        check("cfd_get_jacobi_kernel",
+              load().cfd_get_jacobi_kernel(self._h, C.byref(kind), name, 96))
+        return {"kind": kind.value, "name": name.value.decode()}
+
     @property
     def halo_depth(self) -> int:
         return int(load().cfd_get_halo_depth(self._h))

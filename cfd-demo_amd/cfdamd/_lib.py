@@ -18,7 +18,7 @@ EXPORTS = [
     "cfd_pressure_solve", "cfd_run_phase", "cfd_set_params", "cfd_get_snapshot",
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
-    "cfd_get_kernel_config", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block",
+    "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block",
     "cfd_last_error", "cfd_abi_version", "cfd_destroy",
 ]
 
@@ -105,6 +105,7 @@ def load():
                                  C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
         "cfd_get_halo_depth": (i32, [vp]),
         "cfd_get_kernel_config": (i32, [vp, C.POINTER(i32), C.POINTER(i32)]),
+        "cfd_get_jacobi_kernel": (i32, [vp, C.POINTER(i32), C.c_char_p, C.c_size_t]),
         "cfd_plan_slab": (i32, [C.c_uint64, i32, i32, C.POINTER(C.c_uint64),
                                 C.POINTER(C.c_uint64)]),
         "cfd_plan_sweep": (i32, [i32, i32, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i32),

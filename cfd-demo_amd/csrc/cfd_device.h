@@ -29,6 +29,18 @@ __device__ __forceinline__ float wave_max(float m) {
     return m;
 }
 
+// Publish a non-negative maximum into slot `key` of a spread set (cfd_internal.h).
+__device__ __forceinline__ void publish_max(uint32_t *set, int key, float m) {
+    if (m > 0.0f) atomicMax(&set[(key & (kResSlots - 1)) * kResStride], __float_as_uint(m));
+}
+
+// max(base, every slot of a set); called by all 64 lanes of a wave, uniform result.
+__device__ __forceinline__ float read_max(const uint32_t *set, uint32_t base) {
+    const int lane = (int)threadIdx.x & 63;
+    const float v = lane < kResSlots ? __uint_as_float(set[lane * kResStride]) : 0.0f;
+    return fmaxf(wave_max(v), __uint_as_float(base));
+}
+
 // XCD-aware block order.  The dispatcher deals workgroups to the 8 XCDs
 // round-robin (block b -> XCD b % 8), and each XCD has its own L2; renumber
 // so XCD x works on one contiguous range of tiles (rows), keeping the rows

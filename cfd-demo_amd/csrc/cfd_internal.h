@@ -25,6 +25,16 @@ constexpr int kGhostUV = 2;
 constexpr int kMaxSweeps = 4096;   // per pressure solve
 constexpr int kMaxPasses = 64;     // corrector passes + 1
 
+// Residual maxima are published with atomicMax on f32 bits.  Device-scope
+// atomics on ONE address serialise at the memory side (~10 ns each, measured:
+// 6,000 per launch cost 54 us), so every maximum is spread over kResSlots
+// addresses kResStride words apart and folded by its reader (fold_res /
+// read_res).  Sweep k of a solve owns slots err_slots[(k*kResSlots + s)*kResStride];
+// the 4 step maxima own red_slots likewise.  Slots are zero between uses.
+constexpr int kResSlots = 32;
+constexpr int kResStride = 16;
+constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 4) * kResSlots * kResStride;
+
 // Device-resident control block: every data-dependent decision of
 // Model::update lives here so a whole step can be enqueued (or replayed as a
 // hipGraph) with no host round trip.
@@ -75,6 +85,8 @@ struct Fields {
     float *pp[2];                                      // p' ping-pong
     const uint8_t *mask_u, *mask_v;
     const int32_t *obs;       // (i, j_global) pairs, cells touching this slab
+    uint32_t *err_slots;      // spread per-sweep residual maxima (kResSlots per sweep)
+    uint32_t *red_slots;      // spread step maxima (4 x kResSlots)
     int32_t n_obs;
     size_t u_alloc, v_alloc;  // floats in the u/v allocations (incl. ghosts)
     float *u_alloc_base, *v_alloc_base, *u_old_base, *v_old_base, *u_star_base, *v_star_base;
@@ -90,24 +102,30 @@ void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipSt
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s);
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).
+// res: publish this sweep's residual (always with the tolerance on; only the
+// last sweep of a fixed-count solve needs it).
 void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int row_lo,
-                         int row_hi, hipStream_t s);
+                         int row_hi, int res, hipStream_t s);
 // T consecutive Jacobi sweeps in one launch (temporal blocking, tolerance
 // off): the final sweep's rows [out_lo, out_hi) are stored; sweep `it` of the
 // block is the first.  T <= kMaxTemporal.
 // `par` = launches of this solve before this one (selects the source buffer:
 // buffers flip once per launch).
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
-                         int out_lo, int out_hi, hipStream_t s);
+                         int out_lo, int out_hi, int res, hipStream_t s);
 // The block kernels behind it: k_jacobi_tb (T <= 4, cfd_jacobi_tb1.hip) and
 // the prefetch-pipelined march with 4 or 2 columns per lane (T <= 8,
 // cfd_jacobi_pipe4.hip / cfd_jacobi_pipe2.hip).
+// res_slots: the slot set the last sweep's residual goes to, or null.
 void launch_tb1(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                int out_hi, hipStream_t s);
+                int out_hi, uint32_t *res_slots, hipStream_t s);
 void launch_pipe4(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                  int out_hi, hipStream_t s);
+                  int out_hi, uint32_t *res_slots, hipStream_t s);
 void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                  int out_hi, hipStream_t s);
+                  int out_hi, uint32_t *res_slots, hipStream_t s);
+// dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before
+// an all-reduce of dst reads it).
+void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s);
 // Exhaustive check over all 2^32 f32 inputs x of x/c against the two fast
 // forms; writes mismatch counts {mode1, mode2} to dev_counts (2 x u64).
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s);

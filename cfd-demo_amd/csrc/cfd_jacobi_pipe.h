@@ -234,7 +234,8 @@ struct Pipe {
 template <int T, int FAST, int VEC>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_pipe(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
+    Ctl *ctl, uint32_t *res_slots, int pass, int it, int par, int out_lo, int out_hi, int nwc,
+    int nseg) {
     if (pass_off(ctl, pass)) return;
     using Wv = Pipe<T, FAST, VEC>;
     using L = typename Wv::L;
@@ -322,13 +323,14 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_pipe(
         w.template run<true>();
     else
         w.template run<false>();
+    if (!res_slots) return;
     const float m = wave_max(out_lane ? w.m : 0.0f);
-    if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
+    if (lane == 0) publish_max(res_slots, bid * kJacWavesPerBlock + wave, m);
 }
 
 template <int VEC, int T>
 void launch_pipe_t(const Geom &g, const Fields &f, int pass, int it, int par, int out_lo,
-                   int out_hi, hipStream_t s) {
+                   int out_hi, uint32_t *rs, hipStream_t s) {
     const int nch = g.nx / VEC;
     const int nwc = cdiv(nch, Pipe<T, 1, VEC>::OUTL);
     int nseg;
@@ -344,27 +346,27 @@ void launch_pipe_t(const Geom &g, const Fields &f, int pass, int it, int par, in
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi_pipe<T, 1, VEC>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                           pass, it, par, out_lo, out_hi, nwc, nseg);
+                           rs, pass, it, par, out_lo, out_hi, nwc, nseg);
     else if (g.fastdiv == 2)
         hipLaunchKernelGGL((k_jacobi_pipe<T, 2, VEC>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                           pass, it, par, out_lo, out_hi, nwc, nseg);
+                           rs, pass, it, par, out_lo, out_hi, nwc, nseg);
     else
         hipLaunchKernelGGL((k_jacobi_pipe<T, 0, VEC>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,
-                           pass, it, par, out_lo, out_hi, nwc, nseg);
+                           rs, pass, it, par, out_lo, out_hi, nwc, nseg);
 }
 
 template <int VEC>
 void launch_pipe(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                 int out_hi, hipStream_t s) {
+                 int out_hi, uint32_t *rs, hipStream_t s) {
     switch (T) {
-    case 1: launch_pipe_t<VEC, 1>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 2: launch_pipe_t<VEC, 2>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 3: launch_pipe_t<VEC, 3>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 4: launch_pipe_t<VEC, 4>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 5: launch_pipe_t<VEC, 5>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 6: launch_pipe_t<VEC, 6>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 7: launch_pipe_t<VEC, 7>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    default: launch_pipe_t<VEC, 8>(g, f, pass, it, par, out_lo, out_hi, s); break;
+    case 1: launch_pipe_t<VEC, 1>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 2: launch_pipe_t<VEC, 2>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 3: launch_pipe_t<VEC, 3>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 4: launch_pipe_t<VEC, 4>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 5: launch_pipe_t<VEC, 5>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 6: launch_pipe_t<VEC, 6>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 7: launch_pipe_t<VEC, 7>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    default: launch_pipe_t<VEC, 8>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
     }
 }
 

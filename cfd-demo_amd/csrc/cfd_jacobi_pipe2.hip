@@ -4,7 +4,7 @@
 
 namespace cfd {
 void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                  int out_hi, hipStream_t s) {
-    launch_pipe<2>(g, f, T, pass, it, par, out_lo, out_hi, s);
+                  int out_hi, uint32_t *rs, hipStream_t s) {
+    launch_pipe<2>(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
 }
 }  // namespace cfd

@@ -172,7 +172,8 @@ struct TbWave {
 template <int T, int FAST>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int par, int out_lo, int out_hi, int nwc, int nseg) {
+    Ctl *ctl, uint32_t *res_slots, int pass, int it, int par, int out_lo, int out_hi, int nwc,
+    int nseg) {
     if (pass_off(ctl, pass)) return;
     TbWave<T, FAST> w;
     // the wave index is uniform; readfirstlane lets the compiler see it, so
@@ -245,13 +246,14 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_tb(
         w.template run<true>();
     else
         w.template run<false>();
+    if (!res_slots) return;
     const float m = wave_max(w.out_lane ? w.m : 0.0f);
-    if (w.lane == 0 && m > 0.0f) atomicMax(&ctl->err[it + T - 1], __float_as_uint(m));
+    if (w.lane == 0) publish_max(res_slots, (int)blockIdx.x * kJacWavesPerBlock + wave, m);
 }
 
 template <int T>
 void launch_t(const Geom &g, const Fields &f, int pass, int it, int par, int out_lo, int out_hi,
-              hipStream_t s) {
+              uint32_t *rs, hipStream_t s) {
     const int nch = g.nx / 4;
     const int nwc = cdiv(nch, 62);
     int nseg;
@@ -266,25 +268,25 @@ void launch_t(const Geom &g, const Fields &f, int pass, int it, int par, int out
     const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     if (g.fastdiv == 1)
-        hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, pass,
-                           it, par, out_lo, out_hi, nwc, nseg);
+        hipLaunchKernelGGL((k_jacobi_tb<T, 1>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, rs,
+                           pass, it, par, out_lo, out_hi, nwc, nseg);
     else if (g.fastdiv == 2)
-        hipLaunchKernelGGL((k_jacobi_tb<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, pass,
-                           it, par, out_lo, out_hi, nwc, nseg);
+        hipLaunchKernelGGL((k_jacobi_tb<T, 2>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, rs,
+                           pass, it, par, out_lo, out_hi, nwc, nseg);
     else
-        hipLaunchKernelGGL((k_jacobi_tb<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, pass,
-                           it, par, out_lo, out_hi, nwc, nseg);
+        hipLaunchKernelGGL((k_jacobi_tb<T, 0>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, rs,
+                           pass, it, par, out_lo, out_hi, nwc, nseg);
 }
 
 }  // namespace
 
 void launch_tb1(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                int out_hi, hipStream_t s) {
+                int out_hi, uint32_t *rs, hipStream_t s) {
     switch (T) {
-    case 1: launch_t<1>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 2: launch_t<2>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    case 3: launch_t<3>(g, f, pass, it, par, out_lo, out_hi, s); break;
-    default: launch_t<4>(g, f, pass, it, par, out_lo, out_hi, s); break;
+    case 1: launch_t<1>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 2: launch_t<2>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    case 3: launch_t<3>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
+    default: launch_t<4>(g, f, pass, it, par, out_lo, out_hi, rs, s); break;
     }
 }
 

@@ -280,15 +280,19 @@ __global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pas
 //
 // Residual: max |N - P| over columns 1..=nx-8 only (the reference's full
 // 8-lane chunks; the scalar tail :755-772 never updates max_error), owned
-// rows only, NaN-ignoring like reduce_max.  One atomicMax per wave.
+// rows only, NaN-ignoring like reduce_max.  One atomicMax per wave, into the
+// sweep's spread slot set (only when `res`: a fixed-count solve needs the last
+// sweep's residual alone).
 template <int R, int FAST>
 __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, int pass, int it, int row_lo, int row_hi, int nbx) {
+    Ctl *ctl, uint32_t *slots, int pass, int it, int row_lo, int row_hi, int nbx, int res) {
     if (pass_off(ctl, pass)) return;
     // early exit of the previous sweep (model.rs:816): a skipped sweep leaves
-    // its err slot at 0 so every later sweep of the solve skips too.
-    if (g.tol_enabled && it > 0 && __uint_as_float(ctl->err[it - 1]) < g.p_tol) return;
+    // its slots at 0 so every later sweep of the solve skips too.
+    if (g.tol_enabled && it > 0 &&
+        read_max(slots + (size_t)(it - 1) * kResSlots * kResStride, ctl->err[it - 1]) < g.p_tol)
+        return;
 
     const int nx = g.nx, nch = nx >> 2, hg = g.hg, nyl = g.nyl;
     const int wave = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
@@ -411,8 +415,9 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
         w0 = w4;
         w1 = w5;
     }
+    if (!res) return;
     m = wave_max(m);
-    if (lane == 0 && m > 0.0f) atomicMax(&ctl->err[it], __float_as_uint(m));
+    if (lane == 0) publish_max(slots + (size_t)it * kResSlots * kResStride, bid * kJacWavesPerBlock + wave, m);
 }
 
 // End of a pressure solve: how many sweeps ran, which buffer is current, the
@@ -422,6 +427,18 @@ __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int
                                                            int check_break, int flips) {
     Ctl *c = f.ctl;
     __shared__ int go_s;
+    // fold the spread residual slots into err[]: every sweep's with the
+    // tolerance on, only the last one's for a fixed-count solve (the only
+    // sweep that publishes); one wave per sweep, one lane per slot
+    const int k_lo = g.tol_enabled ? 0 : (iters > 0 ? iters - 1 : 0);
+    const int wv = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+    for (int k = k_lo + wv; k < iters; k += nw) {
+        uint32_t *set = f.err_slots + (size_t)k * kResSlots * kResStride;
+        const float v = read_max(set, c->err[k]);
+        if ((threadIdx.x & 63) < kResSlots) set[(threadIdx.x & 63) * kResStride] = 0u;
+        if ((threadIdx.x & 63) == 0) c->err[k] = __float_as_uint(v);
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         const int go = pass < 0 ? 1 : c->go[pass];
         if (go) {
@@ -445,6 +462,19 @@ __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int
     __syncthreads();
     if (go_s)
         for (int k = threadIdx.x; k < iters; k += blockDim.x) c->err[k] = 0u;
+}
+
+// dst[q] = max(dst[q], slots of set q), then zero the slots (q < n).
+__global__ void k_fold_slots(uint32_t *dst, uint32_t *slots, int n) {
+    const int q = (int)threadIdx.x;
+    if (q >= n) return;
+    uint32_t *set = slots + (size_t)q * kResSlots * kResStride;
+    uint32_t v = dst[q];
+    for (int s = 0; s < kResSlots; ++s) {
+        v = max(v, set[s * kResStride]);
+        set[s * kResStride] = 0u;
+    }
+    dst[q] = v;
 }
 
 // ------------------------------------------------------------- corrector (K5)
@@ -633,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, flo
         float r = 0.f;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) r = fmaxf(r, red[w][threadIdx.x]);
-        if (r > 0.f) atomicMax(&c->red[threadIdx.x], __float_as_uint(r));
+        publish_max(f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride, bid, r);
     }
 }
 
@@ -662,18 +692,29 @@ __global__ __launch_bounds__(kBlock) void k_step_reduce(Geom g, Fields f) {
     mu = wave_max(mu);
     mv = wave_max(mv);
     if ((threadIdx.x & 63) == 0) {
-        uint32_t *r = f.ctl->red;
-        if (du > 0.f) atomicMax(&r[0], __float_as_uint(du));
-        if (dv > 0.f) atomicMax(&r[1], __float_as_uint(dv));
-        if (mu > 0.f) atomicMax(&r[2], __float_as_uint(mu));
-        if (mv > 0.f) atomicMax(&r[3], __float_as_uint(mv));
+        const int key = (int)(tid >> 6);
+        constexpr size_t S = (size_t)kResSlots * kResStride;
+        publish_max(f.red_slots, key, du);
+        publish_max(f.red_slots + S, key, dv);
+        publish_max(f.red_slots + 2 * S, key, mu);
+        publish_max(f.red_slots + 3 * S, key, mv);
     }
 }
 
 // update() epilogue (model.rs:347-377): residuals, step/time, CFL dt.
 __global__ void k_step_finalize(Geom g, Fields f) {
-    if (threadIdx.x != 0) return;
     Ctl *c = f.ctl;
+    if (threadIdx.x < 4) {   // fold the spread step maxima (sharded: already folded)
+        uint32_t *set = f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride;
+        uint32_t v = c->red[threadIdx.x];
+        for (int s = 0; s < kResSlots; ++s) {
+            v = max(v, set[s * kResStride]);
+            set[s * kResStride] = 0u;
+        }
+        c->red[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     c->res_u = __uint_as_float(c->red[0]);
     c->res_v = __uint_as_float(c->red[1]);
     const float max_vel = fmaxf(__uint_as_float(c->red[2]), __uint_as_float(c->red[3]));
@@ -749,7 +790,7 @@ void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_overri
 }
 
 void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int row_lo,
-                         int row_hi, hipStream_t s) {
+                         int row_hi, int res, hipStream_t s) {
     if (row_hi <= row_lo) return;
     const int nch = g.nx / 4;
     const int nwc = cdiv(nch, 64);
@@ -759,24 +800,29 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
     const dim3 grid(nbx * nseg), block(kJacWavesPerBlock * 64);
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi<kJacRowsPerWave, 1>), grid, block, 0, s, g, pa, pb, f.rhs,
-                           f.ctl, pass, it, row_lo, row_hi, nbx);
+                           f.ctl, f.err_slots, pass, it, row_lo, row_hi, nbx, res);
     else if (g.fastdiv == 2)
         hipLaunchKernelGGL((k_jacobi<kJacRowsPerWave, 2>), grid, block, 0, s, g, pa, pb, f.rhs,
-                           f.ctl, pass, it, row_lo, row_hi, nbx);
+                           f.ctl, f.err_slots, pass, it, row_lo, row_hi, nbx, res);
     else
         hipLaunchKernelGGL((k_jacobi<kJacRowsPerWave, 0>), grid, block, 0, s, g, pa, pb, f.rhs,
-                           f.ctl, pass, it, row_lo, row_hi, nbx);
+                           f.ctl, f.err_slots, pass, it, row_lo, row_hi, nbx, res);
 }
 
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
-                         int out_lo, int out_hi, hipStream_t s) {
+                         int out_lo, int out_hi, int res, hipStream_t s) {
     if (out_hi <= out_lo) return;
+    uint32_t *rs = res ? f.err_slots + (size_t)(it + T - 1) * kResSlots * kResStride : nullptr;
     if (g.tb_kind == 3)
-        launch_pipe4(g, f, T, pass, it, par, out_lo, out_hi, s);
+        launch_pipe4(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else if (g.tb_kind == 4)
-        launch_pipe2(g, f, T, pass, it, par, out_lo, out_hi, s);
+        launch_pipe2(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else
-        launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, s);
+        launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
+}
+
+void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_fold_slots, dim3(1), dim3(64), 0, s, dst, slots, n);
 }
 
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s) {

@@ -98,6 +98,7 @@ struct cfd_model {
     uint8_t *mask_u = nullptr, *mask_v = nullptr;
     int32_t *obs = nullptr;
     Ctl *ctl = nullptr;
+    uint32_t *slots = nullptr;   // spread residual maxima (cfd_internal.h kResSlots)
     std::vector<uint8_t> h_mask_u, h_mask_v;
     std::vector<uint8_t> dmask_u, dmask_v;   // staging for the async mask upload
     // sharding
@@ -243,13 +244,15 @@ struct cfd_model {
         if (!sharded()) {
             if (tmax <= 1) {
                 for (int it = 0; it < iters; ++it)
-                    launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g, stream);
+                    launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g,
+                                        g.tol_enabled || it == iters - 1, stream);
                 launches = iters;
             } else {
                 for (int it = 0; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, tmax, iters, &T, &lo, &hi, &exch);
-                    launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, stream);
+                    launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, it + T == iters,
+                                        stream);
                     it += T;
                     ++launches;
                 }
@@ -262,10 +265,11 @@ struct cfd_model {
             for (int it = 0; it < iters;) {
                 int T, lo, hi, exch;
                 plan_block(g.j0, g.nyl, g.ny, g.hg, it, tmax, iters, &T, &lo, &hi, &exch);
+                const int res = it + T == iters;
                 if (tmax == 1)
-                    launch_jacobi_sweep(g, f, pass, it, lo, hi, stream);
+                    launch_jacobi_sweep(g, f, pass, it, lo, hi, res, stream);
                 else
-                    launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, stream);
+                    launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, res, stream);
                 it += T;
                 ++launches;
                 if (exch) {
@@ -273,7 +277,10 @@ struct cfd_model {
                     if (rc) return rc;
                 }
             }
-            int rc = allreduce_max_u32(f.ctl->err + (iters > 0 ? iters - 1 : 0), 1);
+            const int last = iters > 0 ? iters - 1 : 0;
+            launch_fold_slots(f.ctl->err + last, f.err_slots + (size_t)last * kResSlots * kResStride,
+                              1, stream);
+            int rc = allreduce_max_u32(f.ctl->err + last, 1);
             if (rc) return rc;
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
         }
@@ -295,7 +302,9 @@ struct cfd_model {
         const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
         int n = 0;
         for (int it = 0; it < iters; ++it) {
-            launch_jacobi_sweep(g, f, -1, it, lo, hi, stream);
+            launch_jacobi_sweep(g, f, -1, it, lo, hi, 1, stream);
+            launch_fold_slots(f.ctl->err + it, f.err_slots + (size_t)it * kResSlots * kResStride, 1,
+                              stream);
             int rc = allreduce_max_u32(f.ctl->err + it, 1);
             if (rc) return rc;
             rc = exchange_pp((host_cur + it + 1) & 1, 1);
@@ -382,6 +391,7 @@ struct cfd_model {
         rc = enqueue_piso(kNaN, fused);
         if (rc) return rc;
         if (!fused) launch_step_reduce(g, f, stream);
+        if (sharded()) launch_fold_slots(f.ctl->red, f.red_slots, 4, stream);
         rc = allreduce_max_u32(f.ctl->red, 4);
         if (rc) return rc;
         launch_step_finalize(g, f, stream);
@@ -418,7 +428,7 @@ struct cfd_model {
         for (void *ptr : {(void *)u_all, (void *)v_all, (void *)uo_all, (void *)vo_all,
                           (void *)us_all, (void *)vs_all, (void *)p, (void *)rhs,
                           (void *)pp_all[0], (void *)pp_all[1], (void *)mask_u, (void *)mask_v,
-                          (void *)obs, (void *)ctl})
+                          (void *)obs, (void *)ctl, (void *)slots})
             if (ptr) (void)hipFree(ptr);
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (ev_step0) (void)hipEventDestroy(ev_step0);
@@ -549,7 +559,10 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         int rc0 = choose_division(m->stream, g);
         if (rc0) return rc0;
     }
-    g.tb_kind = 1;
+    // kind 4 (prefetch-pipelined march, 2 columns per lane) at T = 4 is the
+    // fastest measured geometry on the bench workload (tools/tune_tb.py, r1:
+    // 8.45 us/sweep vs 11.05 for kind 1 and 11.3 for kind 3 at its best T)
+    g.tb_kind = 4;
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
         g.tb_kind = (k == 3 || k == 4) ? k : 1;
@@ -557,7 +570,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // the pipelined kernels park masked lanes at a far voffset that must not
     // wrap past 2^32 when the row offset is added: slabs up to 1 GiB per field
     if ((uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u > (1ull << 30)) g.tb_kind = 1;
-    m->t_max = g.tb_kind == 1 ? 4 : 6;
+    m->t_max = g.tb_kind == 3 ? 6 : 4;
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
     m->t_max = std::min(m->t_max, g.tb_kind == 1 ? 4 : kMaxTemporal);
     // 24 output rows per wave segment: the best measured geometry at 4096^2
@@ -598,7 +611,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         (rc = zalloc((void **)&m->p, p_n * 4)) || (rc = zalloc((void **)&m->rhs, pp_n * 4)) ||
         (rc = zalloc((void **)&m->pp_all[0], pp_n * 4)) || (rc = zalloc((void **)&m->pp_all[1], pp_n * 4)) ||
         (rc = zalloc((void **)&m->mask_u, nyl * W + 16)) || (rc = zalloc((void **)&m->mask_v, (nyl + 1) * nx + 16)) ||
-        (rc = zalloc((void **)&m->ctl, sizeof(Ctl))))
+        (rc = zalloc((void **)&m->ctl, sizeof(Ctl))) ||
+        (rc = zalloc((void **)&m->slots, kSlotWords * 4)))
         return rc;
 
     // obstacle masks and cell list from cell centres (model.rs:235-260)
@@ -673,6 +687,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.obs = m->obs;
     f.n_obs = (int32_t)(obs.size() / 2);
     f.ctl = m->ctl;
+    f.err_slots = m->slots;
+    f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
 
     Ctl c0;
     std::memset(&c0, 0, sizeof(c0));
@@ -1004,7 +1020,8 @@ int cfd_profile_sweeps(cfd_model *m, int n_sweeps, double *avg_ms_out) {
     Geom g = m->g;
     g.tol_enabled = 0;
     HIP_TRY(hipEventRecord(a, m->stream));
-    for (int it = 0; it < n_sweeps; ++it) launch_jacobi_sweep(g, m->f, -1, it, lo, hi, m->stream);
+    for (int it = 0; it < n_sweeps; ++it)
+        launch_jacobi_sweep(g, m->f, -1, it, lo, hi, it == n_sweeps - 1, m->stream);
     HIP_TRY(hipEventRecord(b, m->stream));
     launch_finalize_solve(g, m->f, -1, n_sweeps, 0, n_sweeps, m->stream);
     HIP_TRY(hipGetLastError());
@@ -1065,6 +1082,24 @@ int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal) {
     if (!m) return fail(CFD_EINVAL, "null model");
     if (fastdiv) *fastdiv = m->g.fastdiv;
     if (temporal) *temporal = m->g.tol_enabled ? 1 : m->t_max;
+    return 0;
+}
+
+int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    const int T = m->g.tol_enabled ? 1 : m->t_max;
+    const int k = T <= 1 ? 0 : m->g.tb_kind;
+    if (kind) *kind = k;
+    if (name && name_len) {
+        char buf[96];
+        if (k == 0)
+            snprintf(buf, sizeof buf, "k_jacobi<%d, %d>", kJacRowsPerWave, m->g.fastdiv);
+        else if (k == 1)
+            snprintf(buf, sizeof buf, "k_jacobi_tb<%d, %d>", T, m->g.fastdiv);
+        else
+            snprintf(buf, sizeof buf, "k_jacobi_pipe<%d, %d, %d>", T, m->g.fastdiv, k == 3 ? 4 : 2);
+        snprintf(name, name_len, "%s", buf);
+    }
     return 0;
 }
 

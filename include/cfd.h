@@ -183,6 +183,12 @@ int cfd_get_halo_depth(const cfd_model *m);
  * for this grid's divisors (0 IEEE, 1 reciprocal multiply, 2 FMA-corrected)
  * and sweeps per launch (1 when the tolerance is on). */
 int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal);
+/* The Jacobi kernel a fixed-count solve launches: kind 0 single sweep
+ * (k_jacobi), 1 register-march temporal blocking (k_jacobi_tb), 3 / 4 the
+ * prefetch-pipelined march with 4 / 2 columns per lane (k_jacobi_pipe), and
+ * its instantiated name as rocprofv3 reports it (NUL-terminated, truncated to
+ * name_len). */
+int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len);
 
 /* Host-only slab plan used by cfd_create_sharded (no device needed; the
  * multi-rank CPU tests drive the same plan):

@@ -14,7 +14,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 m = cfdamd.Model(cfdamd.cavity_grid(n),
                  cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False))
-m.update_n(2)
+m.update_n(int(os.environ.get("TB_WARMUP", "150")))
 m.synchronize()
 m.timing_begin()
 m.update_n(steps)
