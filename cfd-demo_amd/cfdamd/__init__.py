@@ -33,6 +33,7 @@ __all__ = [
     "VelocityScheme", "InletProfile", "PressureSolver", "BoundaryKind", "Cylinder", "Grid",
     "SimulationParams", "Residuals", "SimSnapshot", "Model", "SimulationControlHandle",
     "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "load", "LocalHub",
+    "VisualizationMode",
 ]
 
 
@@ -48,6 +49,12 @@ class InletProfile(enum.IntEnum):            # model.rs:154-159
 
 class PressureSolver(enum.IntEnum):          # model.rs:148-152
     Jacobi = 0
+
+
+class VisualizationMode(enum.IntEnum):       # app.rs:505-509
+    Pressure = 0
+    Velocity = 1
+    Vorticity = 2
 
 
 class BoundaryKind(enum.IntEnum):            # build-defined
@@ -327,6 +334,23 @@ class Model:
         check("cfd_get_kernel_config",
               load().cfd_get_kernel_config(self._h, C.byref(fd), C.byref(tb)))
         return {"fastdiv": fd.value, "temporal": tb.value}
+
+    # -------------------------------------------------------- visualisation
+    def render(self, mode: "VisualizationMode" = VisualizationMode.Pressure):
+        """The image App::update_simulation_view builds (app.rs:235-403),
+        derived on the device: returns (rgba uint8 (nyl, nx, 4), (min, max))."""
+        img = np.empty((self.nyl, self.grid.nx, 4), np.uint8)
+        mm = np.empty(2, np.float32)
+        check("cfd_render", load().cfd_render(
+            self._h, int(mode), img.ctypes.data_as(C.POINTER(C.c_uint8)), _fp(mm)))
+        return img, (float(mm[0]), float(mm[1]))
+
+    def derive_field(self, mode: "VisualizationMode"):
+        """The mode's scalar field (nyl, nx) f32 and its (min, max)."""
+        out = np.empty((self.nyl, self.grid.nx), np.float32)
+        mm = np.empty(2, np.float32)
+        check("cfd_derive_field", load().cfd_derive_field(self._h, int(mode), _fp(out), _fp(mm)))
+        return out, (float(mm[0]), float(mm[1]))
 
     def launches_per_solve(self) -> int:
         """Jacobi launches of one fixed-count solve, from the same host plan

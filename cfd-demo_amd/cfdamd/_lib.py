@@ -19,7 +19,7 @@ EXPORTS = [
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
     "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block",
-    "cfd_last_error", "cfd_abi_version", "cfd_destroy",
+    "cfd_render", "cfd_derive_field", "cfd_last_error", "cfd_abi_version", "cfd_destroy",
 ]
 
 
@@ -113,6 +113,8 @@ def load():
         "cfd_plan_halo": (i32, [i32, i32, i32, i32, i32, C.POINTER(i32)]),
         "cfd_plan_block": (i32, [i32, i32, i32, i32, i32, i32, i32, C.POINTER(i32),
                                  C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+        "cfd_render": (i32, [vp, i32, C.POINTER(C.c_uint8), FP]),
+        "cfd_derive_field": (i32, [vp, i32, FP, FP]),
         "cfd_last_error": (C.c_char_p, []),
         "cfd_abi_version": (i32, []),
         "cfd_destroy": (None, [vp]),

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/cfd.h"
+
 namespace cfd {
 
 constexpr int kGhostUV = 2;
@@ -33,7 +35,7 @@ constexpr int kMaxPasses = 64;     // corrector passes + 1
 // the 4 step maxima own red_slots likewise.  Slots are zero between uses.
 constexpr int kResSlots = 32;
 constexpr int kResStride = 16;
-constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 4) * kResSlots * kResStride;
+constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 8) * kResSlots * kResStride;
 
 // Device-resident control block: every data-dependent decision of
 // Model::update lives here so a whole step can be enqueued (or replayed as a
@@ -48,6 +50,7 @@ struct Ctl {
     float last_p;           // last_pressure_residual
     float res_u, res_v;     // last_u_residual / last_v_residual
     uint32_t red[4];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|
+    uint32_t vis[2];        // render: max key, max ~key of the derived field (cfd_render.hip)
     uint64_t sweeps_total;
     int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
     uint32_t err[kMaxSweeps];        // per-sweep max |p'new - p'| as f32 bits
@@ -87,6 +90,7 @@ struct Fields {
     const int32_t *obs;       // (i, j_global) pairs, cells touching this slab
     uint32_t *err_slots;      // spread per-sweep residual maxima (kResSlots per sweep)
     uint32_t *red_slots;      // spread step maxima (4 x kResSlots)
+    uint32_t *vis_slots;      // spread render min/max keys (2 x kResSlots)
     int32_t n_obs;
     size_t u_alloc, v_alloc;  // floats in the u/v allocations (incl. ghosts)
     float *u_alloc_base, *v_alloc_base, *u_old_base, *v_old_base, *u_star_base, *v_star_base;
@@ -126,6 +130,14 @@ void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int p
 // dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before
 // an all-reduce of dst reads it).
 void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s);
+// Visualisation (cfd_render.hip, src/app.rs:235-403): derived field of `mode`
+// into `out` (may be null) with its min/max keys into 2 spread sets; then the
+// RGBA8 image from the folded keys (field null: re-derive on the fly).
+void launch_vis_field(const Geom &g, const Fields &f, int mode, float *out, uint32_t *slots,
+                      hipStream_t s);
+void launch_vis_color(const Geom &g, const Fields &f, int mode, const float *field, uint32_t *px,
+                      const uint32_t *keys, int has_cyl, float cx, float cy, float radius,
+                      hipStream_t s);
 // Exhaustive check over all 2^32 f32 inputs x of x/c against the two fast
 // forms; writes mismatch counts {mode1, mode2} to dev_counts (2 x u64).
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s);

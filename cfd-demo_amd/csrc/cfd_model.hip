@@ -99,6 +99,7 @@ struct cfd_model {
     int32_t *obs = nullptr;
     Ctl *ctl = nullptr;
     uint32_t *slots = nullptr;   // spread residual maxima (cfd_internal.h kResSlots)
+    float *vis_buf = nullptr;    // render output (nx*nyl words), allocated on first use
     std::vector<uint8_t> h_mask_u, h_mask_v;
     std::vector<uint8_t> dmask_u, dmask_v;   // staging for the async mask upload
     // sharding
@@ -428,7 +429,7 @@ struct cfd_model {
         for (void *ptr : {(void *)u_all, (void *)v_all, (void *)uo_all, (void *)vo_all,
                           (void *)us_all, (void *)vs_all, (void *)p, (void *)rhs,
                           (void *)pp_all[0], (void *)pp_all[1], (void *)mask_u, (void *)mask_v,
-                          (void *)obs, (void *)ctl, (void *)slots})
+                          (void *)obs, (void *)ctl, (void *)slots, (void *)vis_buf})
             if (ptr) (void)hipFree(ptr);
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (ev_step0) (void)hipEventDestroy(ev_step0);
@@ -689,6 +690,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.ctl = m->ctl;
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
+    f.vis_slots = f.red_slots + (size_t)4 * kResSlots * kResStride;
 
     Ctl c0;
     std::memset(&c0, 0, sizeof(c0));
@@ -923,6 +925,67 @@ int cfd_get_snapshot(cfd_model *m, float *u, float *v, float *p, float *dt_out) 
     if (p) HIP_TRY(hipMemcpy(p, m->f.p, nyl * nx * 4, hipMemcpyDeviceToHost));
     if (dt_out) HIP_TRY(hipMemcpy(dt_out, &m->ctl->dt, 4, hipMemcpyDeviceToHost));
     return 0;
+}
+
+namespace {
+
+float decode_key(uint32_t k, bool is_min) {   // inverse of ord_key (cfd_render.hip)
+    if (is_min) {
+        if (!k) return INFINITY;
+        k = ~k;
+    } else if (!k) {
+        return -INFINITY;
+    }
+    const uint32_t b = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    float x;
+    std::memcpy(&x, &b, 4);
+    return x;
+}
+
+// cfd_render / cfd_derive_field: field or image of `mode` for the model's
+// slab, min/max reduced over ranks, one D2H copy of nx*nyl words.
+int render_common(cfd_model *m, int mode, bool field, void *host_out, float *min_max_out) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (mode < CFD_VIS_PRESSURE || mode > CFD_VIS_VORTICITY)
+        return fail(CFD_EINVAL, "unknown visualisation mode");
+    HIP_TRY(hipSetDevice(m->device));
+    const size_t n = (size_t)m->g.nx * (size_t)m->g.nyl;
+    if (!m->vis_buf) HIP_TRY(hipMalloc((void **)&m->vis_buf, n * 4));
+    if (mode == CFD_VIS_VORTICITY) {   // reads u/v one row above the slab
+        int rc = m->exchange_uv();
+        if (rc) return rc;
+    }
+    Fields &f = m->f;
+    launch_vis_field(m->g, f, mode, field ? m->vis_buf : nullptr, f.vis_slots, m->stream);
+    launch_fold_slots(f.ctl->vis, f.vis_slots, 2, m->stream);
+    int rc = m->allreduce_max_u32(f.ctl->vis, 2);
+    if (rc) return rc;
+    const cfd_grid &gr = m->grid;
+    if (!field && host_out)
+        launch_vis_color(m->g, f, mode, nullptr, (uint32_t *)m->vis_buf, f.ctl->vis,
+                         gr.has_cylinder, gr.cylinder_x, gr.cylinder_y, gr.cylinder_radius,
+                         m->stream);
+    HIP_TRY(hipGetLastError());
+    uint32_t keys[2] = {0u, 0u};
+    HIP_TRY(hipMemcpyAsync(keys, f.ctl->vis, 8, hipMemcpyDeviceToHost, m->stream));
+    HIP_TRY(hipMemsetAsync(f.ctl->vis, 0, 8, m->stream));
+    if (host_out) HIP_TRY(hipMemcpyAsync(host_out, m->vis_buf, n * 4, hipMemcpyDeviceToHost, m->stream));
+    HIP_TRY(hipStreamSynchronize(m->stream));
+    if (min_max_out) {
+        min_max_out[0] = decode_key(keys[1], true);
+        min_max_out[1] = decode_key(keys[0], false);
+    }
+    return 0;
+}
+
+}  // namespace
+
+int cfd_render(cfd_model *m, int mode, uint8_t *rgba, float *min_max_out) {
+    return render_common(m, mode, false, rgba, min_max_out);
+}
+
+int cfd_derive_field(cfd_model *m, int mode, float *out, float *min_max_out) {
+    return render_common(m, mode, true, out, min_max_out);
 }
 
 int cfd_get_residuals(cfd_model *m, cfd_residuals *out) {

@@ -209,6 +209,23 @@ int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6
 int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, int iters, int *T,
                    int *out_lo, int *out_hi, int *exchange);
 
+/* Visualisation modes of App (src/app.rs:505-509 VisualizationMode). */
+typedef enum { CFD_VIS_PRESSURE = 0, CFD_VIS_VELOCITY = 1, CFD_VIS_VORTICITY = 2 } cfd_vis_mode;
+
+/* Device-side equivalent of the image App::update_simulation_view builds
+ * from a snapshot (src/app.rs:235-403): derive the mode's scalar field
+ * (p; cell-centred |velocity|; interior vorticity, 0 elsewhere), its min/max
+ * (NaN ignored) and the RGBA8 image (r = (norm*255) as u8, g = 0,
+ * b = ((1-norm)*255) as u8, a = 255; cells whose centre is within the
+ * cylinder radius, `<=`, grey 128), all on the device; only nx*ny*4 bytes
+ * are copied into rgba (row-major, x fastest; NULL skips the image).
+ * min_max_out (2 floats, may be NULL) gets the field's min and max before
+ * the reference's 1e-6 range widening.  Sharded: the rank's slab rows, with
+ * min/max reduced over all ranks (collective: every rank must call). */
+int cfd_render(cfd_model *m, int mode, uint8_t *rgba, float *min_max_out);
+/* The mode's derived scalar field itself (nx*ny f32; slab rows when sharded). */
+int cfd_derive_field(cfd_model *m, int mode, float *out, float *min_max_out);
+
 const char *cfd_last_error(void);
 int cfd_abi_version(void);
 void cfd_destroy(cfd_model *m);

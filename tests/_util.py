@@ -5,13 +5,19 @@ STATE_FIELDS = ("u", "v", "p", "u_star", "v_star", "p_prime")
 
 
 def bits(a):
-    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).ravel()
 
 
-def assert_bitwise(name, got, want):
+def assert_bitwise(name, got, want, nan_equal=False):
+    """Every f32 word identical.  nan_equal: any NaN matches any NaN (the
+    sign/payload of a NaN produced by arithmetic is the hardware's default
+    NaN, not part of the reference's semantics)."""
+    assert np.shape(got) == np.shape(want), f"{name}: shape {np.shape(got)} != {np.shape(want)}"
     g, w = bits(got), bits(want)
-    assert g.shape == w.shape, f"{name}: shape {g.shape} != {w.shape}"
-    bad = np.nonzero(g != w)[0]
+    ne = g != w
+    if nan_equal:
+        ne &= ~(np.isnan(g.view(np.float32)) & np.isnan(w.view(np.float32)))
+    bad = np.nonzero(ne)[0]
     if bad.size:
         k = bad[0]
         raise AssertionError(
