@@ -644,6 +644,25 @@ float orc_auto_dt(const orc_model *m) {
     return fminf(dt_cfl, m->dt);
 }
 
+/* The solve piso_step runs at model.rs:684 / :710 for the selected solver. */
+float orc_pressure_solve(orc_model *m) {
+    if (m->solver == 1) {
+        int n = 0;
+        float r = orc_sor_solve(m->f[ORC_PP], m->f[ORC_RHS], m->nx, m->ny, m->dx, m->dy,
+                                m->jacobi_iters, m->tol_enabled, m->p_tol, &n);
+        m->sweeps_total += (uint64_t)n;
+        m->last_pressure_residual = r;
+        return r;
+    }
+    if (m->solver == 2) {
+        float r = orc_mg_solve(m->f[ORC_PP], m->f[ORC_RHS], (int)m->nx, (int)m->ny, m->dx, m->dy);
+        m->sweeps_total += 1;
+        m->last_pressure_residual = r;
+        return r;
+    }
+    return orc_jacobi_pressure(m);
+}
+
 /* ---------------------------------------------------------------- step */
 
 /* piso_step (model.rs:529-730). */
@@ -651,13 +670,13 @@ void orc_piso_step(orc_model *m, float dt_sub) {
     orc_u_predictor(m, dt_sub);
     orc_v_predictor(m, dt_sub);
     orc_divergence(m, dt_sub);
-    m->last_pressure_residual = orc_jacobi_pressure(m);
+    m->last_pressure_residual = orc_pressure_solve(m);
     orc_corrector(m, dt_sub);
     for (int pass = 0; pass < m->corrector_passes; ++pass) {
         memcpy(m->f[ORC_U_STAR], U_(m), m->len[ORC_U] * sizeof(float));
         memcpy(m->f[ORC_V_STAR], V_(m), m->len[ORC_V] * sizeof(float));
         orc_divergence(m, dt_sub);
-        m->last_pressure_residual = orc_jacobi_pressure(m);
+        m->last_pressure_residual = orc_pressure_solve(m);
         orc_corrector(m, dt_sub);
         if (m->tol_enabled && m->last_pressure_residual < m->p_tol) break; /* :721 */
     }

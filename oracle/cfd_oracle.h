@@ -64,6 +64,23 @@ float orc_jacobi_pressure(orc_model *m);                     /* model.rs:734-824
 void orc_corrector(orc_model *m, float dt_sub);              /* model.rs:1334-1404 */
 void orc_boundary_conditions(orc_model *m);                  /* model.rs:826-875 */
 float orc_auto_dt(const orc_model *m);                       /* model.rs:877-889 */
+/* The solve piso_step runs (model.rs:684, :710) for params.pressure_solver:
+ * 0 Jacobi (model.rs:734-824), 1 red-black SOR, 2 multigrid (the JavaScript
+ * variant's solvers, cfd_oracle_solvers.c).  SOR counts one sweep per
+ * iteration, multigrid one per solve. */
+float orc_pressure_solve(orc_model *m);
+
+/* cfd_oracle_solvers.c — the JavaScript variant's solvers on raw arrays
+ * (index.html:741-795, 1344-1470; double arithmetic, f32 storage). */
+float orc_sor_solve(float *pp, const float *rhs, size_t nx, size_t ny, float dx, float dy,
+                    int iters, int tol_enabled, float p_tol, int *done);
+float orc_mg_solve(float *pp, const float *rhs, int nx, int ny, float dx, float dy);
+void orc_mg_smooth(float *p, const float *rhs, int nx, int ny, double dx, double dy,
+                   int iterations);
+void orc_mg_restrict(const float *fine, int nx_f, int ny_f, float *coarse, int nx_c, int ny_c);
+void orc_mg_prolongate(const float *coarse, int nx_c, int ny_c, float *fine, int nx_f, int ny_f);
+void orc_mg_vcycle(float *p, const float *rhs, int nx, int ny, double dx, double dy);
+float orc_mg_residual(const float *p, const float *rhs, int nx, int ny, double dx, double dy);
 
 /* Raw field access. Field ids: */
 enum { ORC_U = 0, ORC_V, ORC_P, ORC_U_OLD, ORC_V_OLD, ORC_U_STAR, ORC_V_STAR,

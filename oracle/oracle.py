@@ -73,14 +73,74 @@ def lib():
         L.orc_mask.restype = C.POINTER(C.c_uint8)
         L.orc_get_scalars.argtypes = [C.c_void_p, C.POINTER(OrcScalars)]
         L.orc_set_scalars.argtypes = [C.c_void_p, C.POINTER(OrcScalars)]
+        L.orc_pressure_solve.argtypes = [C.c_void_p]
+        L.orc_pressure_solve.restype = C.c_float
+        FP, i32, f64 = C.POINTER(C.c_float), C.c_int, C.c_double
+        L.orc_sor_solve.argtypes = [FP, FP, C.c_size_t, C.c_size_t, C.c_float, C.c_float, i32,
+                                    i32, C.c_float, C.POINTER(i32)]
+        L.orc_sor_solve.restype = C.c_float
+        L.orc_mg_solve.argtypes = [FP, FP, i32, i32, C.c_float, C.c_float]
+        L.orc_mg_solve.restype = C.c_float
+        L.orc_mg_smooth.argtypes = [FP, FP, i32, i32, f64, f64, i32]
+        L.orc_mg_restrict.argtypes = [FP, i32, i32, FP, i32, i32]
+        L.orc_mg_prolongate.argtypes = [FP, i32, i32, FP, i32, i32]
+        L.orc_mg_vcycle.argtypes = [FP, FP, i32, i32, f64, f64]
+        L.orc_mg_residual.argtypes = [FP, FP, i32, i32, f64, f64]
+        L.orc_mg_residual.restype = C.c_float
         _lib = L
     return _lib
 
 
 def make_params(dt=0.005, viscosity=1e-6, target_inlet_velocity=1.0, scheme=0, inlet_profile=0,
-                jacobi_iters=50, corrector_passes=20, tol_enabled=1, p_tol=1e-4, bc_kind=0):
-    return OrcParams(dt, viscosity, target_inlet_velocity, scheme, inlet_profile, 0,
+                jacobi_iters=50, corrector_passes=20, tol_enabled=1, p_tol=1e-4, bc_kind=0,
+                pressure_solver=0):
+    return OrcParams(dt, viscosity, target_inlet_velocity, scheme, inlet_profile, pressure_solver,
                      jacobi_iters, corrector_passes, int(tol_enabled), p_tol, bc_kind)
+
+
+def _fp(a):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+# ---- the JavaScript variant's solvers on raw f32 arrays (cfd_oracle_solvers.c)
+
+def sor_solve(pp, rhs, nx, ny, dx, dy, iters, tol_enabled=True, p_tol=1e-4):
+    """Red-black SOR (index.html:741-774 per-cell formula); pp is overwritten.
+    Returns (residual, iterations run)."""
+    n = C.c_int()
+    r = lib().orc_sor_solve(_fp(pp), _fp(rhs), nx, ny, dx, dy, iters, int(tol_enabled), p_tol,
+                            C.byref(n))
+    return r, n.value
+
+
+def mg_solve(pp, rhs, nx, ny, dx, dy):
+    """Multigrid branch (index.html:775-795): pp = 3 V-cycles from 0; returns the residual."""
+    return lib().orc_mg_solve(_fp(pp), _fp(rhs), nx, ny, dx, dy)
+
+
+def mg_smooth(p, rhs, nx, ny, dx, dy, iterations):
+    lib().orc_mg_smooth(_fp(p), _fp(rhs), nx, ny, dx, dy, iterations)
+
+
+def mg_restrict(fine, nx_f, ny_f, nx_c, ny_c):
+    out = np.empty(nx_c * ny_c, np.float32)
+    lib().orc_mg_restrict(_fp(fine), nx_f, ny_f, _fp(out), nx_c, ny_c)
+    return out
+
+
+def mg_prolongate(coarse, nx_c, ny_c, nx_f, ny_f):
+    out = np.empty(nx_f * ny_f, np.float32)
+    lib().orc_mg_prolongate(_fp(coarse), nx_c, ny_c, _fp(out), nx_f, ny_f)
+    return out
+
+
+def mg_vcycle(p, rhs, nx, ny, dx, dy):
+    lib().orc_mg_vcycle(_fp(p), _fp(rhs), nx, ny, dx, dy)
+
+
+def mg_residual(p, rhs, nx, ny, dx, dy):
+    return lib().orc_mg_residual(_fp(p), _fp(rhs), nx, ny, dx, dy)
 
 
 class OracleModel:
@@ -137,6 +197,10 @@ class OracleModel:
 
     def jacobi(self) -> float:
         return lib().orc_jacobi_pressure(self.h)
+
+    def pressure_solve(self) -> float:
+        """The selected solver (pressure_solver 0 Jacobi, 1 SOR, 2 multigrid)."""
+        return lib().orc_pressure_solve(self.h)
 
     def corrector(self, dt):
         lib().orc_corrector(self.h, dt)
