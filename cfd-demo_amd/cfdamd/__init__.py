@@ -49,6 +49,9 @@ class InletProfile(enum.IntEnum):            # model.rs:154-159
 
 class PressureSolver(enum.IntEnum):          # model.rs:148-152
     Jacobi = 0
+    # the JavaScript variant's solvers (index.html:741-774, 775-795, 1344-1470)
+    Sor = 1
+    Multigrid = 2
 
 
 class VisualizationMode(enum.IntEnum):       # app.rs:505-509
@@ -236,6 +239,11 @@ class Model:
         r = C.c_float()
         check("cfd_pressure_solve", load().cfd_pressure_solve(self._h, C.byref(r)))
         return float(r.value)
+
+    def pressure_solve(self) -> float:
+        """One solve of the selected pressure solver (params.pressure_solver) on
+        the current rhs; returns its residual."""
+        return self.jacobi_pressure()
 
     def run_phase(self, phase: int, dt_sub: float) -> None:
         check("cfd_run_phase", load().cfd_run_phase(self._h, phase, dt_sub))

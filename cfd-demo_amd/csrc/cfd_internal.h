@@ -142,9 +142,47 @@ void launch_vis_color(const Geom &g, const Fields &f, int mode, const float *fie
 // forms; writes mismatch counts {mode1, mode2} to dev_counts (2 x u64).
 void launch_verify_division(float c, float r, unsigned long long *dev_counts, hipStream_t s);
 // flips = launches of a fixed-count solve (ignored with the tolerance on,
-// where each executed sweep is one launch).
+// where each executed sweep is one launch).  exact_flips: flip the current
+// p' buffer exactly `flips` times regardless of the tolerance (solvers that
+// work in place: SOR, multigrid).
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
-                           int flips, hipStream_t s);
+                           int flips, hipStream_t s, int exact_flips = 0);
+
+// ---- alternative pressure solvers (cfd_solvers.hip; index.html) ----
+// Double-precision constants of one grid level: dx2 = dx*dx, dy2 = dy*dy,
+// denom = 2/dx2 + 2/dy2 exactly as the script forms them, their reciprocals,
+// and fast = 1 when all three divisors are powers of two (x / c == x * (1/c)
+// bit for bit for every double x).
+struct SorConst {
+    double dx2, dy2, denom;
+    double r_dx2, r_dy2, r_denom;
+    int32_t fast;
+};
+// One multigrid level: solution ping-pong buffers a/b (level 0: the model's
+// current / other p' buffer), right-hand side, residual scratch, size and the
+// level's constants (spacing 2^l times the model's, index.html:1458).
+struct MgLevel {
+    float *a, *b, *rhs, *r;
+    int32_t nx, ny;
+    double dx2, dy2, denom;
+    double r_dx2, r_dy2, r_denom;
+    int32_t fast;
+};
+constexpr int kMgMaxLevels = 40;
+void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorConst &k, int color,
+                      Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
+                      hipStream_t s);
+void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s);
+void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
+                      hipStream_t s);
+void launch_mg_residual(const MgLevel &L, const float *p, const Ctl *ctl, int pass, hipStream_t s);
+void launch_mg_restrict(const MgLevel &F, const MgLevel &Cl, const Ctl *ctl, int pass, hipStream_t s);
+void launch_mg_prolong_add(const MgLevel &Cl, const float *e, const MgLevel &F, float *p,
+                           const Ctl *ctl, int pass, hipStream_t s);
+void launch_mg_tail(const MgLevel *dev_levels, int s_level, int coarsest, float *a0, float *b0,
+                    const Ctl *ctl, int pass, hipStream_t s);
+void launch_mg_final_residual(const MgLevel &L, const float *p, uint32_t *slots, const Ctl *ctl,
+                              int pass, hipStream_t s);
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s);
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);

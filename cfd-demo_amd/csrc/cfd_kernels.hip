@@ -424,7 +424,8 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
 // returned residual (model.rs:816-823), and whether the corrector loop goes on
 // (model.rs:721-723).  Resets the per-sweep slots for the next solve.
 __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
-                                                           int check_break, int flips) {
+                                                           int check_break, int flips,
+                                                           int exact_flips) {
     Ctl *c = f.ctl;
     __shared__ int go_s;
     // fold the spread residual slots into err[]: every sweep's with the
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int
             const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
             // one buffer flip per launch: per sweep with the tolerance on,
             // `flips` (host-known launch count) for fixed-count solves
-            c->cur = (c->cur + (g.tol_enabled ? n : flips)) & 1;
+            c->cur = (c->cur + ((g.tol_enabled && !exact_flips) ? n : flips)) & 1;
             c->last_p = res;
             c->n_exec_last = (uint32_t)n;
             c->sweeps_total += (uint64_t)n;
@@ -830,9 +831,9 @@ void launch_verify_division(float c, float r, unsigned long long *dev_counts, hi
 }
 
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
-                           int flips, hipStream_t s) {
+                           int flips, hipStream_t s, int exact_flips) {
     hipLaunchKernelGGL(k_finalize_solve, dim3(1), dim3(kBlock), 0, s, g, f, pass, iters,
-                       check_break, flips);
+                       check_break, flips, exact_flips);
 }
 
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,

@@ -118,6 +118,11 @@ struct cfd_model {
     uint64_t timed_sweeps = 0, timed_steps = 0, timed_launches = 0;
     double timed_step_ms = 0.0;
     bool stepped = false;
+    // multigrid hierarchy (cfd_solvers.hip), built on the first multigrid solve
+    std::vector<MgLevel> mg;     // level table; level 0's a/b are the p' buffers of the solve
+    MgLevel *mg_dev = nullptr;   // device copy for k_mg_tail
+    float *mg_pool = nullptr;
+    int mg_tail = 0;             // first level handled inside the single-workgroup tail
 
     bool sharded() const { return n_ranks > 1; }
     size_t u_rows_alloc() const { return (size_t)g.nyl + 2 * kGhostUV; }
@@ -230,7 +235,174 @@ struct cfd_model {
     // (tolerance off): halo depth hg, p' exchanged every hg sweeps; between
     // exchanges each sweep also recomputes a shrinking band of ghost rows, so
     // results equal the single-domain sweep bit for bit.
+    // ------------------------------------------- alternative solvers (index.html)
+    static bool exact_pow2(double c) {
+        int e;
+        return c > 0.0 && std::isfinite(c) && std::frexp(c, &e) == 0.5 && std::isnormal(1.0 / c);
+    }
+
+    // The script's constants for spacing (dx, dy) (index.html:181-183, 1349).
+    static void level_consts(double dx, double dy, double *dx2, double *dy2, double *denom,
+                             double *r, int32_t *fast) {
+        *dx2 = dx * dx;
+        *dy2 = dy * dy;
+        *denom = 2.0 / (dx * dx) + 2.0 / (dy * dy);
+        r[0] = 1.0 / *dx2;
+        r[1] = 1.0 / *dy2;
+        r[2] = 1.0 / *denom;
+        *fast = exact_pow2(*dx2) && exact_pow2(*dy2) && exact_pow2(*denom) ? 1 : 0;
+        if (const char *e = getenv("CFD_FASTDIV"))
+            if (atoi(e) == 0) *fast = 0;
+    }
+
+    void begin_solve_timing(int pass, hipEvent_t *e0) {
+        *e0 = nullptr;
+        if (timing && pass <= 0) {
+            *e0 = take_event();
+            (void)hipEventRecord(*e0, stream);
+        }
+    }
+    void end_solve_timing(hipEvent_t e0, uint64_t sweeps, uint64_t launches) {
+        if (!e0) return;
+        hipEvent_t e1 = take_event();
+        (void)hipEventRecord(e1, stream);
+        solve_events.emplace_back(e0, e1);
+        timed_sweeps += sweeps;
+        timed_launches += launches;
+    }
+
+    // SOR (index.html:741-774) swept red-black, in place on the current p'.
+    int enqueue_sor(int pass) {
+        const int iters = params.jacobi_iters;
+        hipEvent_t e0;
+        begin_solve_timing(pass, &e0);
+        SorConst k;
+        double r[3];
+        level_consts((double)g.dx, (double)g.dy, &k.dx2, &k.dy2, &k.denom, r, &k.fast);
+        k.r_dx2 = r[0];
+        k.r_dy2 = r[1];
+        k.r_denom = r[2];
+        float *pp = f.pp[host_cur];
+        launch_fill_zero(pp, (size_t)g.nx * g.ny, f.ctl, pass, stream);
+        for (int it = 0; it < iters; ++it) {
+            const int res = g.tol_enabled || it == iters - 1;
+            for (int color = 0; color < 2; ++color)
+                launch_sor_color(pp, f.rhs, g.nx, g.ny, k, color, f.ctl, f.err_slots, pass, it,
+                                 g.tol_enabled, g.p_tol, res, stream);
+        }
+        end_solve_timing(e0, (uint64_t)iters, 2 * (uint64_t)iters + 1);
+        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, 0, stream, 1);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+
+    // Level table of mgVcycle's recursion: sizes floor((n+1)/2) down to the
+    // first level with nx <= 4 or ny <= 4 (index.html:1444-1451), spacing
+    // doubling per level (:1458).
+    int mg_build() {
+        if (!mg.empty()) return 0;
+        std::vector<std::pair<int, int>> dims{{g.nx, g.ny}};
+        while (!(dims.back().first <= 4 || dims.back().second <= 4)) {
+            if ((int)dims.size() >= kMgMaxLevels) return fail(CFD_EINVAL, "multigrid: too many levels");
+            dims.push_back({(dims.back().first + 1) / 2, (dims.back().second + 1) / 2});
+        }
+        const int nl = (int)dims.size();
+        size_t total = round4((size_t)g.nx * g.ny);   // level-0 residual
+        for (int l = 1; l < nl; ++l) total += 4 * round4((size_t)dims[l].first * dims[l].second);
+        HIP_TRY(hipMalloc((void **)&mg_pool, total * 4));
+        HIP_TRY(hipMemsetAsync(mg_pool, 0, total * 4, stream));
+        float *cur = mg_pool;
+        auto take = [&](size_t n) {
+            float *p0 = cur;
+            cur += round4(n);
+            return p0;
+        };
+        mg.resize(nl);
+        for (int l = 0; l < nl; ++l) {
+            MgLevel &L = mg[l];
+            std::memset(&L, 0, sizeof(L));
+            L.nx = dims[l].first;
+            L.ny = dims[l].second;
+            const size_t n = (size_t)L.nx * L.ny;
+            if (l == 0) {
+                L.rhs = f.rhs;
+                L.r = take(n);
+            } else {
+                L.a = take(n);
+                L.b = take(n);
+                L.rhs = take(n);
+                L.r = take(n);
+            }
+            const double scale = std::ldexp(1.0, l);   // 2*dx per recursion, exact
+            double r[3];
+            level_consts((double)g.dx * scale, (double)g.dy * scale, &L.dx2, &L.dy2, &L.denom, r,
+                         &L.fast);
+            L.r_dx2 = r[0];
+            L.r_dy2 = r[1];
+            L.r_denom = r[2];
+        }
+        // levels of at most CFD_MG_TAIL cells (default 64 x 64) run inside k_mg_tail
+        long thr = 4096;
+        if (const char *e = getenv("CFD_MG_TAIL")) thr = atol(e);
+        mg_tail = nl - 1;
+        for (int l = 0; l < nl; ++l)
+            if ((long)mg[l].nx * mg[l].ny <= thr) {
+                mg_tail = l;
+                break;
+            }
+        HIP_TRY(hipMalloc((void **)&mg_dev, sizeof(MgLevel) * nl));
+        HIP_TRY(hipMemcpy(mg_dev, mg.data(), sizeof(MgLevel) * nl, hipMemcpyHostToDevice));
+        return 0;
+    }
+
+    // The multigrid branch (index.html:775-795): p' = 0, 3 V-cycles on the
+    // current p' buffer, residual max |A p' - rhs| into the solve's slot set.
+    int enqueue_mg(int pass) {
+        int rc = mg_build();
+        if (rc) return rc;
+        hipEvent_t e0;
+        begin_solve_timing(pass, &e0);
+        const int lc = (int)mg.size() - 1;
+        auto lvl = [&](int l) {
+            MgLevel L = mg[l];
+            if (l == 0) {
+                L.a = f.pp[host_cur];
+                L.b = f.pp[host_cur ^ 1];
+            }
+            return L;
+        };
+        const MgLevel L0 = lvl(0);
+        launch_fill_zero(L0.a, (size_t)g.nx * g.ny, f.ctl, pass, stream);
+        int launches = 1;
+        for (int cycle = 0; cycle < 3; ++cycle) {
+            for (int l = 0; l < mg_tail; ++l) {   // down: 5 smooths a->b, residual, restrict
+                const MgLevel L = lvl(l);
+                for (int t = 0; t < 5; ++t)
+                    launch_mg_smooth(L, t & 1 ? L.b : L.a, t & 1 ? L.a : L.b, f.ctl, pass, stream);
+                launch_mg_residual(L, L.b, f.ctl, pass, stream);
+                launch_mg_restrict(L, lvl(l + 1), f.ctl, pass, stream);
+                launches += 7;
+            }
+            launch_mg_tail(mg_dev, mg_tail, lc, L0.a, L0.b, f.ctl, pass, stream);
+            ++launches;
+            for (int l = mg_tail - 1; l >= 0; --l) {   // up: prolong-add into b, 5 smooths b->a
+                const MgLevel L = lvl(l), Cl = lvl(l + 1);
+                launch_mg_prolong_add(Cl, l + 1 == lc ? Cl.b : Cl.a, L, L.b, f.ctl, pass, stream);
+                for (int t = 0; t < 5; ++t)
+                    launch_mg_smooth(L, t & 1 ? L.a : L.b, t & 1 ? L.b : L.a, f.ctl, pass, stream);
+                launches += 6;
+            }
+        }
+        launch_mg_final_residual(L0, L0.a, f.err_slots, f.ctl, pass, stream);
+        end_solve_timing(e0, 1, (uint64_t)launches + 1);
+        launch_finalize_solve(g, f, pass, 1, pass >= 1 ? 1 : 0, 0, stream, 1);
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+
     int enqueue_solve(int pass) {
+        if (params.pressure_solver == CFD_SOLVER_SOR) return enqueue_sor(pass);
+        if (params.pressure_solver == CFD_SOLVER_MULTIGRID) return enqueue_mg(pass);
         const int iters = params.jacobi_iters;
         const int lo_g = 1 - (int)j0, hi_g = (int)g.ny - 1 - (int)j0;   // global rows 1..ny-2
         bool evt = timing && pass <= 0;
@@ -429,7 +601,8 @@ struct cfd_model {
         for (void *ptr : {(void *)u_all, (void *)v_all, (void *)uo_all, (void *)vo_all,
                           (void *)us_all, (void *)vs_all, (void *)p, (void *)rhs,
                           (void *)pp_all[0], (void *)pp_all[1], (void *)mask_u, (void *)mask_v,
-                          (void *)obs, (void *)ctl, (void *)slots, (void *)vis_buf})
+                          (void *)obs, (void *)ctl, (void *)slots, (void *)vis_buf,
+                          (void *)mg_pool, (void *)mg_dev})
             if (ptr) (void)hipFree(ptr);
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (ev_step0) (void)hipEventDestroy(ev_step0);
@@ -458,7 +631,8 @@ int validate(const cfd_grid *grid, const cfd_params *p) {
         return fail(CFD_EINVAL, "velocity_scheme must be 0 or 1");
     if (p->inlet_profile != 0 && p->inlet_profile != 1)
         return fail(CFD_EINVAL, "inlet_profile must be 0 or 1");
-    if (p->pressure_solver != 0) return fail(CFD_EINVAL, "pressure_solver must be 0 (Jacobi)");
+    if (p->pressure_solver < CFD_SOLVER_JACOBI || p->pressure_solver > CFD_SOLVER_MULTIGRID)
+        return fail(CFD_EINVAL, "pressure_solver must be 0 (Jacobi), 1 (SOR) or 2 (multigrid)");
     if (p->bc_kind != 0 && p->bc_kind != 1) return fail(CFD_EINVAL, "bc_kind must be 0 or 1");
     return 0;
 }
@@ -708,6 +882,8 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     int rc = validate(grid, params);
     if (rc) return rc;
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad rank/n_ranks");
+    if (n_ranks > 1 && params->pressure_solver != CFD_SOLVER_JACOBI)
+        return fail(CFD_EINVAL, "SOR and multigrid solvers run on unsharded models only");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(CFD_EHIP, "no HIP device available");
@@ -900,10 +1076,13 @@ int cfd_set_params(cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
     if (rc) return rc;
+    if (m->sharded() && p->pressure_solver != CFD_SOLVER_JACOBI)
+        return fail(CFD_EINVAL, "SOR and multigrid solvers run on unsharded models only");
     rc = m->sync();
     if (rc) return rc;
-    if (!p->tol_enabled && m->params.tol_enabled) {
-        // host mirror of the current p' buffer is needed again
+    {
+        // host mirror of the current p' buffer (the tolerance-driven Jacobi
+        // solve flips it on the device); fixed-count and in-place solves use it
         Ctl c;
         rc = m->read_ctl(&c);
         if (rc) return rc;

@@ -63,7 +63,14 @@ typedef struct {
  * p_tol 1e-4, bc_kind CFD_BC_CHANNEL. */
 enum { CFD_SCHEME_FIRST_ORDER = 0, CFD_SCHEME_SECOND_ORDER = 1 };
 enum { CFD_INLET_UNIFORM = 0, CFD_INLET_PARABOLIC = 1 };
-enum { CFD_SOLVER_JACOBI = 0 };
+/* Pressure solver of each solve piso_step runs (model.rs:684, :710).
+ * JACOBI is the reference's (model.rs:734-824).  SOR and MULTIGRID are the
+ * solvers of the reference's JavaScript variant (index.html:741-774 and
+ * :775-795 + :1344-1470): p' restarts from 0 each solve, arithmetic in double
+ * with f32 storage as in the script; SOR is swept red-black (omega 1.7,
+ * jacobi_iters iterations, early exit at p_tol); MULTIGRID runs 3 V-cycles and
+ * reports max |A p' - rhs|.  Unsharded models only. */
+enum { CFD_SOLVER_JACOBI = 0, CFD_SOLVER_SOR = 1, CFD_SOLVER_MULTIGRID = 2 };
 enum { CFD_BC_CHANNEL = 0, CFD_BC_CAVITY = 1 };
 typedef struct {
     float dt;

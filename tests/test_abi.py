@@ -88,3 +88,18 @@ def test_invalid_arguments_rejected_before_device():
         with pytest.raises(cfdamd.CfdError) as e:
             cfdamd.Model(g, cfdamd.SimulationParams())
         assert e.value.code == -1
+
+
+def test_solver_choice_validated_before_device():
+    """pressure_solver 0..2; SOR / multigrid are rejected for sharded models."""
+    import cfdamd
+    with pytest.raises(cfdamd.CfdError) as e:
+        cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0),
+                     cfdamd.SimulationParams(pressure_solver=3))
+    assert e.value.code == -1
+    for solver in (cfdamd.PressureSolver.Sor, cfdamd.PressureSolver.Multigrid):
+        with pytest.raises(cfdamd.CfdError) as e:
+            cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0),
+                         cfdamd.SimulationParams(pressure_solver=solver),
+                         n_ranks=2, rank=0, unique_id=bytes(128))
+        assert e.value.code == -1 and "unsharded" in str(e.value)
