@@ -18,9 +18,6 @@ from __future__ import annotations
 
 import ctypes as C
 import enum
-import queue
-import threading
-import time
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -407,78 +404,79 @@ class Model:
 
 
 class SimulationControlHandle:
-    """model.rs:65-117 — command channel into the worker thread plus
-    snapshot / residual channels out of it."""
+    """model.rs:65-117 over the native runtime (cfd_run_*, csrc/cfd_runtime.cpp):
+    a C++ worker thread owns the model and steps it while draining the
+    commands sent here; snapshots and residual records come back through it."""
 
     def __init__(self, model: Model):
-        self._cmd: "queue.Queue" = queue.Queue()
-        self._snap: "queue.Queue" = queue.Queue()
-        self._res: "queue.Queue" = queue.Queue()
         self._model = model
-        self._thread = threading.Thread(target=self._loop, daemon=True)
-        self._thread.start()
+        self._r = C.c_void_p()
+        check("cfd_run_start", load().cfd_run_start(model._h, C.byref(self._r)))
 
-    def _loop(self):                                           # model.rs:1287-1325
-        m, paused, stop = self._model, False, False
-        while not stop:
-            snapshot_sent = False
-            while True:
-                try:
-                    cmd, arg = self._cmd.get_nowait()
-                except queue.Empty:
-                    break
-                if cmd == "stop":
-                    stop = True
-                    break
-                if cmd == "params":
-                    m.set_parameters(arg)
-                elif cmd == "snapshot" and not snapshot_sent:
-                    s = m.get_snapshot()
-                    s.paused = paused
-                    self._snap.put(s)
-                    snapshot_sent = True
-                elif cmd == "pause":
-                    paused = True
-                elif cmd == "resume":
-                    paused = False
-            if stop:
-                break
-            if not paused:
-                m.update()
-                self._res.put(m.get_residuals())
-            else:
-                time.sleep(0.016)
+    def _live(self):
+        if not self._r.value:
+            raise CfdError("cfd_run", -4, "runner stopped")
+        return self._r
 
     def stop(self):
-        self._cmd.put(("stop", None))
+        """Stop and join the worker; the model is usable again afterwards."""
+        if self._r.value:
+            check("cfd_run_stop", load().cfd_run_stop(self._r))
+            self._r = C.c_void_p()
 
     def join(self, timeout=None):
-        self._thread.join(timeout)
+        self.stop()
+
+    def status(self):
+        buf = C.create_string_buffer(256)
+        rc = load().cfd_run_status(self._live(), buf, 256)
+        return rc, buf.value.decode()
+
+    @property
+    def steps(self) -> int:
+        return int(load().cfd_run_steps(self._live()))
 
     def get_last_available_snapshot(self) -> Optional[SimSnapshot]:
-        last = None
-        while True:
-            try:
-                last = self._snap.get_nowait()
-            except queue.Empty:
-                return last
+        su, sv, sp = self._model._sizes()
+        u, v, p = (np.empty(n, np.float32) for n in (su, sv, sp))
+        dt, paused, avail = C.c_float(), C.c_int(), C.c_int()
+        check("cfd_run_last_snapshot", load().cfd_run_last_snapshot(
+            self._live(), _fp(u), _fp(v), _fp(p), C.byref(dt), C.byref(paused), C.byref(avail)))
+        if not avail.value:
+            return None
+        return SimSnapshot(p=p, u=u, v=v, dt=float(dt.value), paused=bool(paused.value))
 
     def get_new_log_messages(self) -> List[Residuals]:
-        out = []
+        out: List[Residuals] = []
+        buf = (CfdResiduals * 256)()
+        n = C.c_int()
         while True:
-            try:
-                out.append(self._res.get_nowait())
-            except queue.Empty:
+            check("cfd_run_new_residuals",
+                  load().cfd_run_new_residuals(self._live(), buf, 256, C.byref(n)))
+            for r in buf[:n.value]:
+                out.append(Residuals(int(r.simulation_step), float(r.simulation_time),
+                                     float(r.dt), float(r.p), float(r.u), float(r.v),
+                                     float(r.step_time_s), int(r.piso_substeps),
+                                     int(r.jacobi_sweeps_total)))
+            if n.value < 256:
                 return out
 
     def request_snapshot(self):
-        self._cmd.put(("snapshot", None))
+        check("cfd_run_request_snapshot", load().cfd_run_request_snapshot(self._live()))
 
     def set_params(self, params: SimulationParams):
-        self._cmd.put(("params", params))
+        p = params._c()
+        check("cfd_run_set_params", load().cfd_run_set_params(self._live(), C.byref(p)))
+        self._model.params = params
 
     def pause(self):
-        self._cmd.put(("pause", None))
+        check("cfd_run_pause", load().cfd_run_pause(self._live()))
 
     def resume(self):
-        self._cmd.put(("resume", None))
+        check("cfd_run_resume", load().cfd_run_resume(self._live()))
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:
+            pass

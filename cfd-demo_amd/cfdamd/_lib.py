@@ -20,6 +20,9 @@ EXPORTS = [
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
     "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block",
     "cfd_render", "cfd_derive_field", "cfd_last_error", "cfd_abi_version", "cfd_destroy",
+    "cfd_get_config", "cfd_run_start", "cfd_run_stop", "cfd_run_pause", "cfd_run_resume",
+    "cfd_run_set_params", "cfd_run_request_snapshot", "cfd_run_last_snapshot",
+    "cfd_run_new_residuals", "cfd_run_status", "cfd_run_steps",
 ]
 
 
@@ -118,6 +121,17 @@ def load():
         "cfd_last_error": (C.c_char_p, []),
         "cfd_abi_version": (i32, []),
         "cfd_destroy": (None, [vp]),
+        "cfd_get_config": (i32, [vp, C.POINTER(CfdGrid), C.POINTER(CfdParams)]),
+        "cfd_run_start": (i32, [vp, C.POINTER(vp)]),
+        "cfd_run_stop": (i32, [vp]),
+        "cfd_run_pause": (i32, [vp]),
+        "cfd_run_resume": (i32, [vp]),
+        "cfd_run_set_params": (i32, [vp, C.POINTER(CfdParams)]),
+        "cfd_run_request_snapshot": (i32, [vp]),
+        "cfd_run_last_snapshot": (i32, [vp, FP, FP, FP, FP, C.POINTER(i32), C.POINTER(i32)]),
+        "cfd_run_new_residuals": (i32, [vp, C.POINTER(CfdResiduals), i32, C.POINTER(i32)]),
+        "cfd_run_status": (i32, [vp, C.c_char_p, C.c_size_t]),
+        "cfd_run_steps": (C.c_uint64, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -175,12 +175,16 @@ void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorCons
 void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
                       hipStream_t s);
+// Five smoothing sweeps src -> dst in one launch (LDS temporal blocking).
+void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
+                       hipStream_t s);
 void launch_mg_residual(const MgLevel &L, const float *p, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_restrict(const MgLevel &F, const MgLevel &Cl, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_prolong_add(const MgLevel &Cl, const float *e, const MgLevel &F, float *p,
                            const Ctl *ctl, int pass, hipStream_t s);
+// fast: the hierarchy's division form (uniform: 2^l scaling keeps powers of two)
 void launch_mg_tail(const MgLevel *dev_levels, int s_level, int coarsest, float *a0, float *b0,
-                    const Ctl *ctl, int pass, hipStream_t s);
+                    int fast, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_final_residual(const MgLevel &L, const float *p, uint32_t *slots, const Ctl *ctl,
                               int pass, hipStream_t s);
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,

@@ -373,24 +373,36 @@ struct cfd_model {
         };
         const MgLevel L0 = lvl(0);
         launch_fill_zero(L0.a, (size_t)g.nx * g.ny, f.ctl, pass, stream);
+        // 5 smooths x -> y: one temporally blocked launch, or 5 single sweeps
+        // ping-ponging x/y (CFD_MG_TB=0; the result lands in y either way)
+        const char *tbe = getenv("CFD_MG_TB");
+        const bool tb = !(tbe && atoi(tbe) == 0);
         int launches = 1;
+        auto smooth5 = [&](const MgLevel &L, float *x, float *y) {
+            if (tb) {
+                launch_mg_smooth5(L, x, y, f.ctl, pass, stream);
+                launches += 1;
+            } else {
+                for (int t = 0; t < 5; ++t)
+                    launch_mg_smooth(L, t & 1 ? y : x, t & 1 ? x : y, f.ctl, pass, stream);
+                launches += 5;
+            }
+        };
         for (int cycle = 0; cycle < 3; ++cycle) {
             for (int l = 0; l < mg_tail; ++l) {   // down: 5 smooths a->b, residual, restrict
                 const MgLevel L = lvl(l);
-                for (int t = 0; t < 5; ++t)
-                    launch_mg_smooth(L, t & 1 ? L.b : L.a, t & 1 ? L.a : L.b, f.ctl, pass, stream);
+                smooth5(L, L.a, L.b);
                 launch_mg_residual(L, L.b, f.ctl, pass, stream);
                 launch_mg_restrict(L, lvl(l + 1), f.ctl, pass, stream);
-                launches += 7;
+                launches += 2;
             }
-            launch_mg_tail(mg_dev, mg_tail, lc, L0.a, L0.b, f.ctl, pass, stream);
+            launch_mg_tail(mg_dev, mg_tail, lc, L0.a, L0.b, L0.fast, f.ctl, pass, stream);
             ++launches;
             for (int l = mg_tail - 1; l >= 0; --l) {   // up: prolong-add into b, 5 smooths b->a
                 const MgLevel L = lvl(l), Cl = lvl(l + 1);
                 launch_mg_prolong_add(Cl, l + 1 == lc ? Cl.b : Cl.a, L, L.b, f.ctl, pass, stream);
-                for (int t = 0; t < 5; ++t)
-                    launch_mg_smooth(L, t & 1 ? L.a : L.b, t & 1 ? L.b : L.a, f.ctl, pass, stream);
-                launches += 6;
+                smooth5(L, L.b, L.a);
+                launches += 1;
             }
         }
         launch_mg_final_residual(L0, L0.a, f.err_slots, f.ctl, pass, stream);
@@ -939,6 +951,16 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
 extern "C" {
 
 const char *cfd_last_error(void) { return g_last_error.c_str(); }
+// internal (not in cfd.h): lets the host runtime (cfd_runtime.cpp) report
+// through the same thread-local message
+void cfdrt_set_error(const char *msg) { g_last_error = msg ? msg : ""; }
+
+int cfd_get_config(const cfd_model *m, cfd_grid *grid, cfd_params *params) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (grid) *grid = m->grid;
+    if (params) *params = m->params;
+    return 0;
+}
 int cfd_abi_version(void) { return CFD_ABI_VERSION; }
 
 void cfd_default_params(cfd_params *o) {

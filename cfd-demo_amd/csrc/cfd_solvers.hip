@@ -24,8 +24,13 @@
 namespace cfd {
 namespace {
 
-__device__ __forceinline__ double ddiv(double x, double c, double r, int fast) {
-    return fast ? x * r : x / c;
+// x / c in the script's double arithmetic.  FAST is a template parameter:
+// with a runtime flag the compiler if-converts and evaluates the ~30-instruction
+// IEEE f64 division sequence on both paths.
+template <int FAST>
+__device__ __forceinline__ double ddiv(double x, double c, double r) {
+    if (FAST) return x * r;
+    return x / c;
 }
 
 // ------------------------------------------------------------------- SOR
@@ -40,6 +45,7 @@ __device__ __forceinline__ double ddiv(double x, double c, double r, int fast) {
 // script's result after its row loop then its column loop.  Every cell that
 // reads a boundary value (column 0 / nx-1, row 0 / ny-1) is updated by the
 // same thread that later stores that boundary value.
+template <int FAST>
 __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
                                                       const float *__restrict__ rhs, int nx, int ny,
                                                       SorConst k, int color, Ctl *ctl,
@@ -62,9 +68,9 @@ __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
         if (i >= 1 && i <= nx - 2) {
             const long idx = row + i;
             const double p_old = (double)(i == i0 ? c.x : c.y);
-            const double h = ddiv((double)pp[idx + 1] + (double)pp[idx - 1], k.dx2, k.r_dx2, k.fast);
-            const double v = ddiv((double)pp[idx + nx] + (double)pp[idx - nx], k.dy2, k.r_dy2, k.fast);
-            const double p_update = ddiv(h + v - (double)rhs[idx], k.denom, k.r_denom, k.fast);
+            const double h = ddiv<FAST>((double)pp[idx + 1] + (double)pp[idx - 1], k.dx2, k.r_dx2);
+            const double v = ddiv<FAST>((double)pp[idx + nx] + (double)pp[idx - nx], k.dy2, k.r_dy2);
+            const double p_update = ddiv<FAST>(h + v - (double)rhs[idx], k.denom, k.r_denom);
             const double omega = 1.7;
             const float nv = (float)((1.0 - omega) * p_old + omega * p_update);
             m = (float)fabs((double)nv - p_old);
@@ -99,6 +105,7 @@ __global__ __launch_bounds__(kBlock) void k_fill_zero(float4 *p, long n4, const 
 // mgSmooth (index.html:1351-1359), one sweep: interior cells get the Jacobi
 // value, boundary cells are copied (the script leaves them in place; here the
 // sweep ping-pongs between two buffers).
+template <int FAST>
 __device__ __forceinline__ void mg_smooth_cell(const MgLevel &L, const float *__restrict__ src,
                                                float *__restrict__ dst, int i, int j) {
     const int nx = L.nx;
@@ -109,12 +116,13 @@ __device__ __forceinline__ void mg_smooth_cell(const MgLevel &L, const float *__
     }
     const double p_e = src[idx + 1], p_w = src[idx - 1];
     const double p_n = src[idx + nx], p_s = src[idx - nx];
-    const double h = ddiv(p_e + p_w, L.dx2, L.r_dx2, L.fast);
-    const double v = ddiv(p_n + p_s, L.dy2, L.r_dy2, L.fast);
-    dst[idx] = (float)ddiv(h + v - (double)L.rhs[idx], L.denom, L.r_denom, L.fast);
+    const double h = ddiv<FAST>(p_e + p_w, L.dx2, L.r_dx2);
+    const double v = ddiv<FAST>(p_n + p_s, L.dy2, L.r_dy2);
+    dst[idx] = (float)ddiv<FAST>(h + v - (double)L.rhs[idx], L.denom, L.r_denom);
 }
 
 // r = rhs - A p on the interior, 0 on the boundary (index.html:1430-1441).
+template <int FAST>
 __device__ __forceinline__ void mg_residual_cell(const MgLevel &L, const float *__restrict__ p,
                                                  int i, int j) {
     const int nx = L.nx;
@@ -124,8 +132,8 @@ __device__ __forceinline__ void mg_residual_cell(const MgLevel &L, const float *
         return;
     }
     const double p_e = p[idx + 1], p_w = p[idx - 1], p_n = p[idx + nx], p_s = p[idx - nx];
-    const double ap = ddiv(p_e + p_w, L.dx2, L.r_dx2, L.fast) +
-                      ddiv(p_n + p_s, L.dy2, L.r_dy2, L.fast) - L.denom * (double)p[idx];
+    const double ap = ddiv<FAST>(p_e + p_w, L.dx2, L.r_dx2) +
+                      ddiv<FAST>(p_n + p_s, L.dy2, L.r_dy2) - L.denom * (double)p[idx];
     L.r[idx] = (float)((double)L.rhs[idx] - ap);
 }
 
@@ -175,19 +183,96 @@ __device__ __forceinline__ void mg_prolong_add_cell(const MgLevel &Cl, const flo
     p[idx] = (float)((double)p[idx] + (double)(float)val);
 }
 
+// Five mgSmooth sweeps in one launch (temporal blocking): a block owns a
+// window of kSmW columns x kSmH rows of p and rhs — its kSmW - 2T output
+// columns by kSmTH output rows plus T halo cells on every side — and runs the
+// T sweeps on it on-chip, storing the output tile once, so p and rhs cross HBM
+// once per T sweeps instead of T times.  Each thread owns one window column
+// in registers (p, rhs; vertical neighbours are register neighbours, the
+// unrolled row loop keeps every index static); only the column exchange with
+// the neighbouring threads goes through LDS (ping-pong, one barrier per
+// sweep).  Cells whose dependency cone leaves the window compute garbage that
+// no valid cell reads: after sweep s the window minus s cells on each side is
+// exact, so the output tile is exact after T.  Every sweep is the
+// single-sweep arithmetic of mg_smooth_cell, so results are identical.
+constexpr int kSmT = 5;                    // sweeps per launch (mgVcycle pre/post-smooth, :1427, :1469)
+constexpr int kSmW = 256;                  // window columns = threads per block
+constexpr int kSmOW = kSmW - 2 * kSmT;     // output columns per block
+// output rows per block: tall tiles (less halo recompute) on big levels,
+// short ones (shorter serial row march per block) on small levels
+constexpr int kSmTHBig = 30, kSmTHSmall = 14;
+
+template <int FAST, int kSmTH>
+__global__ __launch_bounds__(kSmW) void k_mg_smooth5(MgLevel L, const float *__restrict__ src,
+                                                     float *__restrict__ dst, const Ctl *ctl,
+                                                     int pass, int nbx) {
+    constexpr int kSmH = kSmTH + 2 * kSmT;     // window rows
+    if (pass_off(ctl, pass)) return;
+    __shared__ float xch[2][kSmH][kSmW];
+    const int x = (int)threadIdx.x;
+    const int gx0 = ((int)blockIdx.x % nbx) * kSmOW - kSmT;   // window origin (global)
+    const int gy0 = ((int)blockIdx.x / nbx) * kSmTH - kSmT;
+    const int nx = L.nx, ny = L.ny;
+    const int gx = gx0 + x;
+    const bool col_in = gx >= 0 && gx < nx;
+    const bool bcol = gx == 0 || gx == nx - 1;
+    const int xl = x > 0 ? x - 1 : 0, xr = x < kSmW - 1 ? x + 1 : kSmW - 1;
+    float c[kSmH];
+    double rh[kSmH];
+#pragma unroll
+    for (int y = 0; y < kSmH; ++y) {
+        const int gy = gy0 + y;
+        const bool in = col_in && gy >= 0 && gy < ny;
+        const long k = (long)gy * nx + gx;
+        c[y] = in ? src[k] : 0.0f;
+        rh[y] = in ? (double)L.rhs[k] : 0.0;
+        xch[0][y][x] = c[y];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kSmT; ++s) {
+        const int cur = s & 1;
+        // rows top-down in place: `below` keeps the old value of row y-1
+        double below = (double)c[0];
+#pragma unroll
+        for (int y = 1; y < kSmH - 1; ++y) {
+            const int gy = gy0 + y;
+            const double here = (double)c[y];
+            if (!(bcol || gy <= 0 || gy >= ny - 1)) {
+                const double h = ddiv<FAST>((double)xch[cur][y][xr] + (double)xch[cur][y][xl],
+                                            L.dx2, L.r_dx2);
+                const double vt = ddiv<FAST>((double)c[y + 1] + below, L.dy2, L.r_dy2);
+                c[y] = (float)ddiv<FAST>(h + vt - rh[y], L.denom, L.r_denom);
+            }
+            below = here;
+            if (s + 1 < kSmT) xch[cur ^ 1][y][x] = c[y];
+        }
+        if (s + 1 < kSmT) __syncthreads();
+    }
+    if (col_in && x >= kSmT && x < kSmW - kSmT) {
+#pragma unroll
+        for (int y = kSmT; y < kSmH - kSmT; ++y) {
+            const int gy = gy0 + y;
+            if (gy < ny) dst[(long)gy * nx + gx] = c[y];
+        }
+    }
+}
+
 // Grid-wide passes: one cell per thread, nbx blocks per row.
+template <int FAST>
 __global__ __launch_bounds__(kBlock) void k_mg_smooth(MgLevel L, const float *src, float *dst,
                                                       const Ctl *ctl, int pass, int nbx) {
     if (pass_off(ctl, pass)) return;
     const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x, j = (int)blockIdx.x / nbx;
-    if (i < L.nx) mg_smooth_cell(L, src, dst, i, j);
+    if (i < L.nx) mg_smooth_cell<FAST>(L, src, dst, i, j);
 }
 
+template <int FAST>
 __global__ __launch_bounds__(kBlock) void k_mg_residual(MgLevel L, const float *p, const Ctl *ctl,
                                                         int pass, int nbx) {
     if (pass_off(ctl, pass)) return;
     const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x, j = (int)blockIdx.x / nbx;
-    if (i < L.nx) mg_residual_cell(L, p, i, j);
+    if (i < L.nx) mg_residual_cell<FAST>(L, p, i, j);
 }
 
 __global__ __launch_bounds__(kBlock) void k_mg_restrict(MgLevel F, MgLevel Cl, const Ctl *ctl,
@@ -213,6 +298,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_prolong_add(MgLevel Cl, const flo
 // buffers (the model's current / other p' buffer).
 constexpr int kTailThreads = 1024;
 
+template <int FAST>
 __global__ __launch_bounds__(kTailThreads) void k_mg_tail(const MgLevel *__restrict__ lv, int s,
                                                           int lc, float *a0, float *b0,
                                                           const Ctl *ctl, int pass) {
@@ -229,7 +315,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_tail(const MgLevel *__restr
     auto smooth_n = [&](const MgLevel &L, float *x, float *y, int n) {
         const int cells = L.nx * L.ny;
         for (int t = 0; t < n; ++t) {
-            for (int k = tid; k < cells; k += kTailThreads) mg_smooth_cell(L, x, y, k % L.nx, k / L.nx);
+            for (int k = tid; k < cells; k += kTailThreads) mg_smooth_cell<FAST>(L, x, y, k % L.nx, k / L.nx);
             __syncthreads();
             float *tmp = x;
             x = y;
@@ -239,7 +325,7 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_tail(const MgLevel *__restr
     for (int l = s; l < lc; ++l) {
         const MgLevel L = level(l), Cl = level(l + 1);
         smooth_n(L, L.a, L.b, 5);
-        for (int k = tid; k < L.nx * L.ny; k += kTailThreads) mg_residual_cell(L, L.b, k % L.nx, k / L.nx);
+        for (int k = tid; k < L.nx * L.ny; k += kTailThreads) mg_residual_cell<FAST>(L, L.b, k % L.nx, k / L.nx);
         __syncthreads();
         for (int k = tid; k < Cl.nx * Cl.ny; k += kTailThreads) mg_restrict_cell(L, Cl, k % Cl.nx, k / Cl.nx);
         __syncthreads();
@@ -263,22 +349,36 @@ __global__ __launch_bounds__(kTailThreads) void k_mg_tail(const MgLevel *__restr
 
 // Final residual of the multigrid branch (index.html:783-795): max |A p - rhs|
 // over the interior, NaN ignored, published as f32 into a spread slot set.
+// A block walks a band of `rows` rows (one column per thread) and publishes
+// one maximum: per-wave atomics over a 4096^2 grid would serialise.
+template <int FAST>
 __global__ __launch_bounds__(kBlock) void k_mg_final_residual(MgLevel L, const float *p,
                                                               uint32_t *slots, const Ctl *ctl,
-                                                              int pass, int nbx) {
+                                                              int pass, int nbx, int rows) {
     if (pass_off(ctl, pass)) return;
-    const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x, j = (int)blockIdx.x / nbx;
+    __shared__ float wmax[kBlock / 64];
+    const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
+    const int jb = ((int)blockIdx.x / nbx) * rows;
     const int nx = L.nx;
     float m = 0.0f;
-    if (i >= 1 && i <= nx - 2 && j >= 1 && j <= L.ny - 2) {
-        const long idx = (long)j * nx + i;
-        const double r = ddiv((double)p[idx + 1] + (double)p[idx - 1], L.dx2, L.r_dx2, L.fast) +
-                         ddiv((double)p[idx + nx] + (double)p[idx - nx], L.dy2, L.r_dy2, L.fast) -
-                         L.denom * (double)p[idx] - (double)L.rhs[idx];
-        m = (float)fabs(r);
+    if (i >= 1 && i <= nx - 2) {
+        const int j1 = min(jb + rows, L.ny - 1);
+        for (int j = max(jb, 1); j < j1; ++j) {
+            const long idx = (long)j * nx + i;
+            const double r = ddiv<FAST>((double)p[idx + 1] + (double)p[idx - 1], L.dx2, L.r_dx2) +
+                             ddiv<FAST>((double)p[idx + nx] + (double)p[idx - nx], L.dy2, L.r_dy2) -
+                             L.denom * (double)p[idx] - (double)L.rhs[idx];
+            m = fmaxf(m, (float)fabs(r));
+        }
     }
     m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) publish_max(slots, (int)blockIdx.x * (kBlock / 64) + ((int)threadIdx.x >> 6), m);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = wmax[0];
+        for (int w = 1; w < kBlock / 64; ++w) b = fmaxf(b, wmax[w]);
+        publish_max(slots, (int)blockIdx.x, b);
+    }
 }
 
 inline int grid_of(int nx, int ny, int *nbx) {
@@ -295,8 +395,12 @@ void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorCons
                       hipStream_t s) {
     if (ny < 3) return;
     const int nbx = cdiv(nx / 2, kBlock);
-    hipLaunchKernelGGL(k_sor_color, dim3(nbx * (ny - 2)), dim3(kBlock), 0, s, pp, rhs, nx, ny, k,
-                       color, ctl, err_slots, pass, it, tol, p_tol, res, nbx);
+    if (k.fast)
+        hipLaunchKernelGGL(k_sor_color<1>, dim3(nbx * (ny - 2)), dim3(kBlock), 0, s, pp, rhs, nx, ny,
+                           k, color, ctl, err_slots, pass, it, tol, p_tol, res, nbx);
+    else
+        hipLaunchKernelGGL(k_sor_color<0>, dim3(nbx * (ny - 2)), dim3(kBlock), 0, s, pp, rhs, nx, ny,
+                           k, color, ctl, err_slots, pass, it, tol, p_tol, res, nbx);
 }
 
 void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s) {
@@ -309,13 +413,35 @@ void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl 
                       hipStream_t s) {
     int nbx;
     const int g = grid_of(L.nx, L.ny, &nbx);
-    hipLaunchKernelGGL(k_mg_smooth, dim3(g), dim3(kBlock), 0, s, L, src, dst, ctl, pass, nbx);
+    if (L.fast)
+        hipLaunchKernelGGL(k_mg_smooth<1>, dim3(g), dim3(kBlock), 0, s, L, src, dst, ctl, pass, nbx);
+    else
+        hipLaunchKernelGGL(k_mg_smooth<0>, dim3(g), dim3(kBlock), 0, s, L, src, dst, ctl, pass, nbx);
+}
+
+void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
+                       hipStream_t s) {
+    const int nbx = cdiv(L.nx, kSmOW);
+    const bool big = (long)L.nx * L.ny >= (1L << 23);
+    const int nby = cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+    const dim3 grid(nbx * nby), block(kSmW);
+    if (L.fast && big)
+        hipLaunchKernelGGL((k_mg_smooth5<1, kSmTHBig>), grid, block, 0, s, L, src, dst, ctl, pass, nbx);
+    else if (L.fast)
+        hipLaunchKernelGGL((k_mg_smooth5<1, kSmTHSmall>), grid, block, 0, s, L, src, dst, ctl, pass, nbx);
+    else if (big)
+        hipLaunchKernelGGL((k_mg_smooth5<0, kSmTHBig>), grid, block, 0, s, L, src, dst, ctl, pass, nbx);
+    else
+        hipLaunchKernelGGL((k_mg_smooth5<0, kSmTHSmall>), grid, block, 0, s, L, src, dst, ctl, pass, nbx);
 }
 
 void launch_mg_residual(const MgLevel &L, const float *p, const Ctl *ctl, int pass, hipStream_t s) {
     int nbx;
     const int g = grid_of(L.nx, L.ny, &nbx);
-    hipLaunchKernelGGL(k_mg_residual, dim3(g), dim3(kBlock), 0, s, L, p, ctl, pass, nbx);
+    if (L.fast)
+        hipLaunchKernelGGL(k_mg_residual<1>, dim3(g), dim3(kBlock), 0, s, L, p, ctl, pass, nbx);
+    else
+        hipLaunchKernelGGL(k_mg_residual<0>, dim3(g), dim3(kBlock), 0, s, L, p, ctl, pass, nbx);
 }
 
 void launch_mg_restrict(const MgLevel &F, const MgLevel &Cl, const Ctl *ctl, int pass, hipStream_t s) {
@@ -332,16 +458,25 @@ void launch_mg_prolong_add(const MgLevel &Cl, const float *e, const MgLevel &F, 
 }
 
 void launch_mg_tail(const MgLevel *dev_levels, int s_level, int coarsest, float *a0, float *b0,
-                    const Ctl *ctl, int pass, hipStream_t s) {
-    hipLaunchKernelGGL(k_mg_tail, dim3(1), dim3(kTailThreads), 0, s, dev_levels, s_level, coarsest,
-                       a0, b0, ctl, pass);
+                    int fast, const Ctl *ctl, int pass, hipStream_t s) {
+    if (fast)
+        hipLaunchKernelGGL(k_mg_tail<1>, dim3(1), dim3(kTailThreads), 0, s, dev_levels, s_level,
+                           coarsest, a0, b0, ctl, pass);
+    else
+        hipLaunchKernelGGL(k_mg_tail<0>, dim3(1), dim3(kTailThreads), 0, s, dev_levels, s_level,
+                           coarsest, a0, b0, ctl, pass);
 }
 
 void launch_mg_final_residual(const MgLevel &L, const float *p, uint32_t *slots, const Ctl *ctl,
                               int pass, hipStream_t s) {
-    int nbx;
-    const int g = grid_of(L.nx, L.ny, &nbx);
-    hipLaunchKernelGGL(k_mg_final_residual, dim3(g), dim3(kBlock), 0, s, L, p, slots, ctl, pass, nbx);
+    const int nbx = cdiv(L.nx, kBlock);
+    const int rows = 32;
+    if (L.fast)
+        hipLaunchKernelGGL(k_mg_final_residual<1>, dim3(nbx * cdiv(L.ny, rows)), dim3(kBlock), 0, s,
+                           L, p, slots, ctl, pass, nbx, rows);
+    else
+        hipLaunchKernelGGL(k_mg_final_residual<0>, dim3(nbx * cdiv(L.ny, rows)), dim3(kBlock), 0, s,
+                           L, p, slots, ctl, pass, nbx, rows);
 }
 
 }  // namespace cfd

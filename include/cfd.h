@@ -233,6 +233,40 @@ int cfd_render(cfd_model *m, int mode, uint8_t *rgba, float *min_max_out);
 /* The mode's derived scalar field itself (nx*ny f32; slab rows when sharded). */
 int cfd_derive_field(cfd_model *m, int mode, float *out, float *min_max_out);
 
+/* The grid and parameters the model runs with (NULL skips either). */
+int cfd_get_config(const cfd_model *m, cfd_grid *grid, cfd_params *params);
+
+/* ---- Model::run (model.rs:1282-1332): the asynchronous host runtime ----
+ * cfd_run_start hands the model to a worker thread that loops exactly as the
+ * reference's (model.rs:1287-1325): drain the queued commands in order
+ * (Stop, SetParams, GetSnapshot — at most one snapshot per drain —, Pause,
+ * Resume; model.rs:57-63), then either run one cfd_update and queue its
+ * residuals, or wait 16 ms while paused.  Until cfd_run_stop returns, only
+ * cfd_run_* calls may touch the model.  Any thread may call cfd_run_*.
+ * Difference: Stop ends the worker (the reference's Stop only leaves the
+ * command loop, model.rs:1296); cfd_run_stop joins it, frees the runner and
+ * leaves the model to the caller. */
+typedef struct cfd_runner cfd_runner;
+int cfd_run_start(cfd_model *m, cfd_runner **out);             /* Model::run        :1282 */
+int cfd_run_stop(cfd_runner *r);                               /* handle.stop()     :72   */
+int cfd_run_pause(cfd_runner *r);                              /* handle.pause()    :110  */
+int cfd_run_resume(cfd_runner *r);                             /* handle.resume()   :114  */
+int cfd_run_set_params(cfd_runner *r, const cfd_params *p);    /* handle.set_params :104  */
+int cfd_run_request_snapshot(cfd_runner *r);                   /* request_snapshot  :100  */
+/* get_last_available_snapshot (:76-86): the newest snapshot published since
+ * the previous call (slab sizes as cfd_get_snapshot; NULL skips a field);
+ * *available = 0 when there is none. */
+int cfd_run_last_snapshot(cfd_runner *r, float *u, float *v, float *p, float *dt_out,
+                          int *paused_out, int *available);
+/* get_new_log_messages (:88-98): up to `max` queued residual records, oldest
+ * first; *n_out = records copied. */
+int cfd_run_new_residuals(cfd_runner *r, cfd_residuals *out, int max, int *n_out);
+/* 0 while the worker is healthy, else the first failing status of a call it
+ * made (it then stops stepping and waits for Stop); msg gets the message. */
+int cfd_run_status(cfd_runner *r, char *msg, size_t msg_len);
+/* Steps the worker has completed. */
+uint64_t cfd_run_steps(cfd_runner *r);
+
 const char *cfd_last_error(void);
 int cfd_abi_version(void);
 void cfd_destroy(cfd_model *m);

@@ -35,12 +35,16 @@ def _oracle(nx, ny, lx, ly, cylinder=None, **p):
     return OracleModel(nx, ny, lx, ly, cylinder=cylinder, **p)
 
 
-@pytest.mark.parametrize("tail", ["default", "0", "100000000"])
+@pytest.mark.parametrize("tail,tb", [("default", "1"), ("0", "1"), ("100000000", "1"),
+                                     ("0", "0")])
 @pytest.mark.parametrize("name", sorted(JS))
-def test_multigrid_solve_matches_reference_javascript(monkeypatch, name, tail):
+def test_multigrid_solve_matches_reference_javascript(monkeypatch, name, tail, tb):
+    """tail: levels run in the single-workgroup tail (0: only the coarsest);
+    tb: five smoothing sweeps per launch through LDS (1) or one per launch (0)."""
     c = _cfd()
     if tail != "default":
         monkeypatch.setenv("CFD_MG_TAIL", tail)
+    monkeypatch.setenv("CFD_MG_TB", tb)
     meta = JS[name]
     fx = np.load(os.path.join(GOLD, name + ".npz"))
     nx, ny = meta["nx"], meta["ny"]
@@ -49,7 +53,7 @@ def test_multigrid_solve_matches_reference_javascript(monkeypatch, name, tail):
     m.set_state(rhs=fx["in_rhs"], p_prime=np.full(nx * ny, 7.0, np.float32))
     r = m.pressure_solve()
     st = m.get_state()
-    assert_bitwise(f"{name} tail={tail}: p'", st["p_prime"], fx["out_solve"])
+    assert_bitwise(f"{name} tail={tail} tb={tb}: p'", st["p_prime"], fx["out_solve"])
     assert np.float32(r) == np.float32(fx["out_residual_f64"][0])
     assert st["jacobi_sweeps_total"] == 1
 
@@ -133,3 +137,22 @@ def test_switching_solvers_mid_run():
     st = m.get_state()
     for f in ("u", "v", "p", "p_prime"):
         assert_bitwise(f, st[f], o.field(f))
+
+
+@pytest.mark.parametrize("nx,ny,lx,ly", [(1024, 1024, 1.0, 1.0), (1048, 1000, 30.0, 10.0)])
+def test_multigrid_large_grids_match_oracle(nx, ny, lx, ly):
+    """Grids of >= 2^20 cells: deep hierarchies, many smoothing tiles and deep
+    hierarchies (power-of-two divisors and IEEE double division)."""
+    c = _cfd()
+    import oracle
+    rng = np.random.default_rng(nx)
+    rhs = (rng.uniform(-1, 1, nx * ny) * 50.0).astype(np.float32)
+    m = c.Model(c.Grid(nx, ny, lx, ly),
+                c.SimulationParams(pressure_solver=c.PressureSolver.Multigrid))
+    m.set_state(rhs=rhs)
+    r = m.pressure_solve()
+    want = np.empty(nx * ny, np.float32)
+    dx, dy = np.float32(lx) / np.float32(nx), np.float32(ly) / np.float32(ny)
+    r2 = oracle.mg_solve(want, rhs, nx, ny, dx, dy)
+    assert_bitwise(f"mg {nx}x{ny}", m.get_state()["p_prime"], want)
+    assert np.float32(r) == np.float32(r2)
