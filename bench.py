@@ -222,6 +222,11 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "traffic_source": traffic_src,
+                # the PMC-measured bytes of this kernel over the same launch time
+                "measured_hbm_GBps": (traffic / (launch_ms * 1e-3) / 1e9
+                                      if traffic and launch_ms > 0 else None),
+                "measured_hbm_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                      if traffic and launch_ms > 0 else None),
                 "kernel": kern["name"], "sweeps_per_launch": T,
                 "avg_launch_us": launch_ms * 1e3,
                 "algorithmic_bytes_per_launch": bytes_launch,
