@@ -23,6 +23,15 @@ EXPORTS = [
     "cfd_get_config", "cfd_run_start", "cfd_run_stop", "cfd_run_pause", "cfd_run_resume",
     "cfd_run_set_params", "cfd_run_request_snapshot", "cfd_run_last_snapshot",
     "cfd_run_new_residuals", "cfd_run_status", "cfd_run_steps",
+    "cfd_polygon_new", "cfd_polygon_new_rect", "cfd_polygon_new_regular", "cfd_polygon_add_hole",
+    "cfd_polygon_contains_point", "cfd_polygon_intersects_aabb",
+    "cfd_polygon_edges_intersect_aabb", "cfd_polygon_bounding_box",
+    "cfd_polygon_bounding_square", "cfd_polygon_edges", "cfd_polygon_destroy",
+    "cfd_geom_do_intersect", "cfd_geom_segment_intersection", "cfd_geom_intersect_quad_edge",
+    "cfd_tesselate", "cfd_quadtree_size", "cfd_quadtree_nodes", "cfd_quadtree_destroy",
+    "cfd_mesh_from_quadtree", "cfd_mesh_sizes", "cfd_mesh_cells", "cfd_mesh_neighbors",
+    "cfd_mesh_intersections", "cfd_mesh_full_bounding_box", "cfd_mesh_build_ms",
+    "cfd_mesh_destroy",
 ]
 
 
@@ -56,6 +65,14 @@ class CfdState(C.Structure):
                 ("simulation_step", C.c_uint64), ("last_p_residual", C.c_float),
                 ("last_u_residual", C.c_float), ("last_v_residual", C.c_float),
                 ("jacobi_sweeps_total", C.c_uint64)]
+
+
+class CfdPoint(C.Structure):
+    _fields_ = [("x", C.c_double), ("y", C.c_double)]
+
+
+class CfdAabb(C.Structure):
+    _fields_ = [("center", CfdPoint), ("half_width", C.c_double), ("half_height", C.c_double)]
 
 
 class CfdError(RuntimeError):
@@ -132,6 +149,37 @@ def load():
         "cfd_run_new_residuals": (i32, [vp, C.POINTER(CfdResiduals), i32, C.POINTER(i32)]),
         "cfd_run_status": (i32, [vp, C.c_char_p, C.c_size_t]),
         "cfd_run_steps": (C.c_uint64, [vp]),
+        # quadtree mesher
+        "cfd_polygon_new": (i32, [C.POINTER(CfdPoint), C.c_size_t, C.POINTER(C.c_uint64),
+                                  C.c_size_t, C.POINTER(vp), C.POINTER(i32)]),
+        "cfd_polygon_new_rect": (i32, [C.c_double] * 4 + [C.POINTER(vp)]),
+        "cfd_polygon_new_regular": (i32, [CfdPoint, C.c_double, C.c_size_t, C.c_double,
+                                          C.POINTER(vp)]),
+        "cfd_polygon_add_hole": (i32, [vp, vp, C.POINTER(i32)]),
+        "cfd_polygon_contains_point": (i32, [vp, CfdPoint, C.POINTER(i32)]),
+        "cfd_polygon_intersects_aabb": (i32, [vp, C.POINTER(CfdAabb), C.POINTER(i32)]),
+        "cfd_polygon_edges_intersect_aabb": (i32, [vp, C.POINTER(CfdAabb), C.POINTER(i32)]),
+        "cfd_polygon_bounding_box": (i32, [vp, C.POINTER(CfdAabb)]),
+        "cfd_polygon_bounding_square": (i32, [vp, C.POINTER(CfdAabb)]),
+        "cfd_polygon_edges": (i32, [vp, C.POINTER(CfdPoint), C.c_size_t, C.POINTER(C.c_size_t)]),
+        "cfd_polygon_destroy": (None, [vp]),
+        "cfd_geom_do_intersect": (i32, [CfdPoint] * 4 + [C.POINTER(i32)]),
+        "cfd_geom_segment_intersection": (i32, [CfdPoint] * 4 + [C.POINTER(CfdPoint),
+                                                                 C.POINTER(i32)]),
+        "cfd_geom_intersect_quad_edge": (i32, [CfdPoint, C.c_double, C.c_double, CfdPoint,
+                                               CfdPoint, C.POINTER(CfdPoint), C.POINTER(i32)]),
+        "cfd_tesselate": (i32, [vp, C.c_double, C.c_double, C.POINTER(vp)]),
+        "cfd_quadtree_size": (i32, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "cfd_quadtree_nodes": (i32, [vp, C.POINTER(CfdAabb), C.POINTER(C.c_int64)]),
+        "cfd_quadtree_destroy": (None, [vp]),
+        "cfd_mesh_from_quadtree": (i32, [vp, vp, i32, C.POINTER(vp)]),
+        "cfd_mesh_sizes": (i32, [vp, C.POINTER(C.c_uint64)]),
+        "cfd_mesh_cells": (i32, [vp] + [C.POINTER(C.c_double)] * 4),
+        "cfd_mesh_neighbors": (i32, [vp, i32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "cfd_mesh_intersections": (i32, [vp, C.POINTER(C.c_uint64), C.POINTER(CfdPoint)]),
+        "cfd_mesh_full_bounding_box": (i32, [vp, C.POINTER(CfdAabb)]),
+        "cfd_mesh_build_ms": (i32, [vp, C.POINTER(C.c_double)]),
+        "cfd_mesh_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

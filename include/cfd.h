@@ -267,6 +267,75 @@ int cfd_run_status(cfd_runner *r, char *msg, size_t msg_len);
 /* Steps the worker has completed. */
 uint64_t cfd_run_steps(cfd_runner *r);
 
+/* ---- the adaptive quadtree mesher (src/quad_mesh, src/utils/intersection.rs) ----
+ * f64 throughout, as the reference.  Polygon construction, the geometry
+ * predicates and the tesselation are host code; Mesh::from_quad_tree
+ * (mesh.rs:51-227: leaf filtering, the O(n^2) face-neighbour search, the
+ * cell/edge intersections) runs on the GPU.  Geometry calls return 0 / a
+ * negative cfd_status like every entry point; the reference's PolygonError
+ * comes back through *poly_error. */
+typedef struct { double x, y; } cfd_point;                    /* point.rs */
+typedef struct { cfd_point center; double half_width, half_height; } cfd_aabb;   /* aabb.rs */
+enum { CFD_POLY_OK = 0, CFD_POLY_NOT_ENOUGH_VERTICES = 1, CFD_POLY_SELF_INTERSECTING = 2,
+       CFD_POLY_INVALID_HOLE = 3 };                          /* PolygonError polygon.rs:12-16 */
+typedef struct cfd_polygon cfd_polygon;
+typedef struct cfd_quadtree cfd_quadtree;
+typedef struct cfd_mesh cfd_mesh;
+
+/* Polygon::new (polygon.rs:19-40): *out is NULL when *poly_error != 0. */
+int cfd_polygon_new(const cfd_point *vertex_buffer, size_t n_points, const uint64_t *vertices,
+                    size_t n_vertices, cfd_polygon **out, int *poly_error);
+int cfd_polygon_new_rect(double x, double y, double w, double h, cfd_polygon **out); /* :42-53 */
+int cfd_polygon_new_regular(cfd_point center, double radius, size_t n, double start_angle,
+                            cfd_polygon **out);                                  /* new_polygon :55-67 */
+/* add_hole (:69-79): on success the polygon takes ownership of `hole`. */
+int cfd_polygon_add_hole(cfd_polygon *p, cfd_polygon *hole, int *poly_error);
+/* contains_point (:81-103), intersects_aabb (:105-117), edges_intersect_aabb
+ * (:119-133): *result 0 / 1. */
+int cfd_polygon_contains_point(const cfd_polygon *p, cfd_point pt, int *result);
+int cfd_polygon_intersects_aabb(const cfd_polygon *p, const cfd_aabb *box, int *result);
+int cfd_polygon_edges_intersect_aabb(const cfd_polygon *p, const cfd_aabb *box, int *result);
+int cfd_polygon_bounding_box(const cfd_polygon *p, cfd_aabb *out);               /* :150-178 */
+int cfd_polygon_bounding_square(const cfd_polygon *p, cfd_aabb *out);            /* :180-184 */
+/* edges (:186-196), reference quirk kept: edge k joins vertex_buffer[v_k] and
+ * vertex_buffer[(v_k + 1) % n_vertices]; out gets 2 points per edge. */
+int cfd_polygon_edges(const cfd_polygon *p, cfd_point *out, size_t max_edges, size_t *n_edges);
+void cfd_polygon_destroy(cfd_polygon *p);
+
+/* utils/intersection.rs: do_intersect (:20-38), line_segment_intersection
+ * (:41-63; *found 0 for None), intersect_quad_edge (:68-129) for
+ * quad = Quad::new_rect(center, hw, hh) (quad.rs:24-35; up to 8 points). */
+int cfd_geom_do_intersect(cfd_point p, cfd_point q, cfd_point a, cfd_point b, int *result);
+int cfd_geom_segment_intersection(cfd_point p, cfd_point q, cfd_point a, cfd_point b,
+                                  cfd_point *out, int *found);
+int cfd_geom_intersect_quad_edge(cfd_point center, double hw, double hh, cfd_point p1,
+                                 cfd_point p2, cfd_point *out8, int *n);
+
+/* tesselate (quad_tree.rs:17-100).  Nodes in depth-first pre-order; children
+ * (4 per node, quadrant order of :43-91) as node indices, -1 for a leaf. */
+int cfd_tesselate(const cfd_polygon *p, double feature_size, double max_cell_size,
+                  cfd_quadtree **out);
+int cfd_quadtree_size(const cfd_quadtree *t, uint64_t *n_nodes, uint64_t *n_leaves);
+int cfd_quadtree_nodes(const cfd_quadtree *t, cfd_aabb *boxes, int64_t *children4);
+void cfd_quadtree_destroy(cfd_quadtree *t);
+
+/* Mesh::from_quad_tree (mesh.rs:51-227) on HIP device `device`.  Arrays as the
+ * reference's SoA Mesh; neighbour lists of each cell in ascending cell order. */
+enum { CFD_FACE_EAST = 0, CFD_FACE_WEST = 1, CFD_FACE_NORTH = 2, CFD_FACE_SOUTH = 3 };
+int cfd_mesh_from_quadtree(const cfd_quadtree *t, const cfd_polygon *p, int device,
+                           cfd_mesh **out);
+/* sizes[0] cells, [1..4] neighbour index counts (east, west, north, south),
+ * [5] intersection points. */
+int cfd_mesh_sizes(const cfd_mesh *m, uint64_t *sizes6);
+int cfd_mesh_cells(const cfd_mesh *m, double *cx, double *cy, double *hw, double *hh);
+/* ranges: 2 x u64 (start, end) per cell. */
+int cfd_mesh_neighbors(const cfd_mesh *m, int face, uint64_t *ranges, uint64_t *indexes);
+int cfd_mesh_intersections(const cfd_mesh *m, uint64_t *ranges, cfd_point *points);
+int cfd_mesh_full_bounding_box(const cfd_mesh *m, cfd_aabb *out);               /* :294-338 */
+/* device time of the last cfd_mesh_from_quadtree's kernels (HIP events) */
+int cfd_mesh_build_ms(const cfd_mesh *m, double *ms);
+void cfd_mesh_destroy(cfd_mesh *m);
+
 const char *cfd_last_error(void);
 int cfd_abi_version(void);
 void cfd_destroy(cfd_model *m);
