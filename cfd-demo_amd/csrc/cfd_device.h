@@ -81,6 +81,15 @@ __device__ __forceinline__ float fdiv(float x, float c, float r) {
     return x / c;
 }
 
+// x / c for a grid spacing c (dx, dy, dx*dx, dy*dy).  SP: every spacing is an
+// exact power of two with a normal reciprocal (Geom::sp_pow2, checked on the
+// host), so x * (1/c) is the correctly rounded value of the same real number
+// as x / c — bit-identical for every x, including subnormals, infinities and NaN.
+template <int SP>
+__device__ __forceinline__ float sdiv(float x, float c, float r) {
+    return SP ? x * r : x / c;
+}
+
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int FAST>

@@ -80,6 +80,10 @@ struct Geom {
     int32_t tb_kind;      // 1: k_jacobi_tb (T <= 4); prefetch pipeline (T <= 8) with
                           // 3: 4 columns per lane, 4: 2 columns per lane
     int32_t xcd_remap;    // renumber blocks so each XCD gets contiguous tiles (xcd_block)
+    // reciprocals of dx, dy, dx*dx, dy*dy; sp_pow2 = 1 when all four spacings
+    // are exact powers of two (then sdiv multiplies, bit-identically)
+    float r_dx, r_dy, r_dxx, r_dyy;
+    int32_t sp_pow2;
 };
 
 struct Fields {
@@ -103,6 +107,8 @@ void launch_step_begin(const Geom &g, const Fields &f, int copy, hipStream_t s);
 void launch_copy_star(const Geom &g, const Fields &f, int pass, hipStream_t s);
 void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+// u and v predictors in one pass (same results as the two launches above).
+void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s);
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).

@@ -78,26 +78,31 @@ __global__ __launch_bounds__(kBlock) void k_copy_star(Fields f, int pass) {
     copy4(f.v_star_base, f.v_alloc_base, f.v_alloc / 4, tid, stride);
 }
 
+// Stencil access for the predictors: U(di, dj) / V(di, dj) are the u / v
+// values at flat offset (di, dj) from the cell — flat row-major indexing, so
+// the reference's wrap-around reads across row ends (U(nx+1, j) == U(0, j+1))
+// come out as they do in model.rs.
+struct GAcc {
+    const float *u, *v;
+    long c, cv;
+    int W, nx;
+    __device__ __forceinline__ float U(int di, int dj) const { return u[c + di + (long)dj * W]; }
+    __device__ __forceinline__ float V(int di, int dj) const { return v[cv + di + (long)dj * nx]; }
+};
+
 // ---------------------------------------------------------- u predictor (K1)
 
 // u* on global rows 1..=ny-2, faces 1..=nx (model.rs:538-580 + compute_ustar
 // :382-436).  One thread per face; neighbour reuse comes from L1/L2.  Flux
 // velocities are the raw v values (get_v_north/south :1056-1069).
-template <int SCHEME>
-__global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float dt_override,
-                                                        int row_lo, int nbx) {
-    const int bid = xcd_block(g);
-    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
-    const int lj = row_lo + bid / nbx;
+template <int SCHEME, int SP, class A>
+__device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, float dt_override,
+                                            int i, int lj, const A &a) {
     const int nx = g.nx, ny = g.ny, W = nx + 1;
-    if (i > nx) return;
     const int j = g.j0 + lj;
-    const float *__restrict__ u = f.u;
-    const float *__restrict__ v = f.v;
     const long c = (long)lj * W + i;
-    const long cv = (long)lj * nx + i;
-    const float uc = u[c], ue1 = u[c + 1], uw1 = u[c - 1], un1 = u[c + W], us1 = u[c - W];
-    const float vn = v[cv + nx], vs = v[cv];
+    const float uc = a.U(0, 0), ue1 = a.U(1, 0), uw1 = a.U(-1, 0), un1 = a.U(0, 1), us1 = a.U(0, -1);
+    const float vn = a.V(0, 1), vs = a.V(0, 0);
     float ue, uw, un, us;
     if (SCHEME == 0) {
         // u_face_{e,w,n,s}_first_order (:893-908, :929-941, :966-981, :1011-1026)
@@ -109,31 +114,31 @@ __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float 
         const size_t ulen = (size_t)W * (size_t)ny;
         // u_face_e_second_order (:911-926)
         if (uc >= 0.0f) {
-            ue = (i > 1) ? 1.5f * uc - 0.5f * u[c - 1] : uc;
+            ue = (i > 1) ? 1.5f * uc - 0.5f * a.U(-1, 0) : uc;
         } else if (((size_t)(i + 1) + (size_t)j * W) + 1 < ulen && i < nx - 1) {
-            ue = 1.5f * ue1 - 0.5f * u[c + 2];
+            ue = 1.5f * ue1 - 0.5f * a.U(2, 0);
         } else {
             ue = ue1;
         }
         // u_face_w_second_order (:944-963)
         if (uw1 >= 0.0f) {
-            uw = (i > 2) ? 1.5f * uw1 - 0.5f * u[c - 2] : uw1;
+            uw = (i > 2) ? 1.5f * uw1 - 0.5f * a.U(-2, 0) : uw1;
         } else {
             uw = (i < nx) ? 1.5f * uc - 0.5f * ue1 : uc;
         }
         // u_face_n_second_order (:992-1008), decision on averaged v (:983-989)
-        const float vnb = 0.5f * (v[cv + nx - 1] + v[cv + nx]);
+        const float vnb = 0.5f * (a.V(-1, 1) + a.V(0, 1));
         if (vnb >= 0.0f) {
             un = (j > 1) ? 1.5f * uc - 0.5f * us1 : uc;
         } else if ((size_t)i + (size_t)(j + 2) * W < ulen && j < ny - 1) {
-            un = 1.5f * un1 - 0.5f * u[c + 2 * W];
+            un = 1.5f * un1 - 0.5f * a.U(0, 2);
         } else {
             un = un1;
         }
         // u_face_s_second_order (:1037-1053), decision on averaged v (:1028-1034)
-        const float vsb = 0.5f * (v[cv - 1] + v[cv]);
+        const float vsb = 0.5f * (a.V(-1, 0) + a.V(0, 0));
         if (vsb >= 0.0f) {
-            us = (j > 1) ? 1.5f * us1 - 0.5f * u[c - 2 * W] : us1;
+            us = (j > 1) ? 1.5f * us1 - 0.5f * a.U(0, -2) : us1;
         } else if (j < ny) {
             us = 1.5f * uc - 0.5f * un1;
         } else {
@@ -146,11 +151,23 @@ __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float 
     const float f_w = uw * uw;
     const float f_n = vn * un;
     const float f_s = vs * us;
-    const float convective = (f_e - f_w) / dx + (f_n - f_s) / dy;
-    const float laplace = (ue1 - 2.0f * uc + uw1) / (dx * dx) + (un1 - 2.0f * uc + us1) / (dy * dy);
+    const float convective = sdiv<SP>(f_e - f_w, dx, g.r_dx) + sdiv<SP>(f_n - f_s, dy, g.r_dy);
+    const float laplace = sdiv<SP>(ue1 - 2.0f * uc + uw1, dx * dx, g.r_dxx) +
+                          sdiv<SP>(un1 - 2.0f * uc + us1, dy * dy, g.r_dyy);
     float r = uc + dt * (-convective + nu * laplace);
     if (f.mask_u[(long)lj * W + i] & 1) r = 0.0f;
-    f.u_star[c] = r;
+    return r;
+}
+
+template <int SCHEME, int SP>
+__global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float dt_override,
+                                                        int row_lo, int nbx) {
+    const int bid = xcd_block(g);
+    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + bid / nbx;
+    if (i > g.nx) return;
+    const GAcc a{f.u, f.v, (long)lj * (g.nx + 1) + i, (long)lj * g.nx + i, g.nx + 1, g.nx};
+    f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
 }
 
 // ---------------------------------------------------------- v predictor (K2)
@@ -159,21 +176,14 @@ __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float 
 // compute_vstar :439-521).  Advecting u is the raw face value U(i+1,j),
 // U(i,j).  SecondOrder: the lane of column nx-1 is never filled (:647-650),
 // so all six inputs are 0.0 there.
-template <int SCHEME>
-__global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float dt_override,
-                                                        int row_lo, int nbx) {
-    const int bid = xcd_block(g);
-    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
-    const int lj = row_lo + bid / nbx;
-    const int nx = g.nx, ny = g.ny, W = nx + 1;
-    if (i > nx - 1) return;
+template <int SCHEME, int SP, class A>
+__device__ __forceinline__ float v_pred_val(const Geom &g, const Fields &f, float dt_override,
+                                            int i, int lj, const A &a) {
+    const int nx = g.nx, ny = g.ny;
     const int j = g.j0 + lj;
-    const float *__restrict__ u = f.u;
-    const float *__restrict__ v = f.v;
     const long cv = (long)lj * nx + i;
-    const long cu = (long)lj * W + i;
-    const float vc = v[cv], ve1 = v[cv + 1], vw1 = v[cv - 1], vn1 = v[cv + nx], vs1 = v[cv - nx];
-    float uE = u[cu + 1], uW = u[cu];
+    const float vc = a.V(0, 0), ve1 = a.V(1, 0), vw1 = a.V(-1, 0), vn1 = a.V(0, 1), vs1 = a.V(0, -1);
+    float uE = a.U(1, 0), uW = a.U(0, 0);
     float ve, vw, vn, vs;
     if (SCHEME == 0) {
         // v_face_{e,w,n,s}_first_order(_scalar) (:1073-1095, :1116-1142, :1163-1185, :1207-1229)
@@ -192,13 +202,13 @@ __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float 
         if (uE >= 0.0f) {
             ve = (i > 0) ? 1.5f * vc - 0.5f * vw1 : vc;
         } else if (idx + 2 < vlen && i < nx - 2) {
-            ve = 1.5f * ve1 - 0.5f * v[cv + 2];
+            ve = 1.5f * ve1 - 0.5f * a.V(2, 0);
         } else {
             ve = ve1;
         }
         // v_face_w_second_order (:1145-1160)
         if (uW >= 0.0f) {
-            vw = (i > 1) ? 1.5f * vw1 - 0.5f * v[cv - 2] : vw1;
+            vw = (i > 1) ? 1.5f * vw1 - 0.5f * a.V(-2, 0) : vw1;
         } else {
             vw = (i < nx - 1) ? 1.5f * vc - 0.5f * ve1 : vc;
         }
@@ -206,13 +216,13 @@ __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float 
         if (0.5f * (vc + vn1) >= 0.0f) {
             vn = (j > 1) ? 1.5f * vc - 0.5f * vs1 : vc;
         } else if ((size_t)i + (size_t)(j + 2) * nx < vlen && j < ny - 1) {
-            vn = 1.5f * vn1 - 0.5f * v[cv + 2 * nx];
+            vn = 1.5f * vn1 - 0.5f * a.V(0, 2);
         } else {
             vn = vn1;
         }
         // v_face_s_second_order (:1232-1248)
         if (0.5f * (vs1 + vc) >= 0.0f) {
-            vs = (j > 1) ? 1.5f * vs1 - 0.5f * v[cv - 2 * nx] : vs1;
+            vs = (j > 1) ? 1.5f * vs1 - 0.5f * a.V(0, -2) : vs1;
         } else if (j < ny) {
             vs = 1.5f * vc - 0.5f * vn1;
         } else {
@@ -229,33 +239,72 @@ __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float 
         const float f_w = uW * vw;
         const float f_n = vn * vn;
         const float f_s = vs * vs;
-        const float convective = (f_e - f_w) / dx + (f_n - f_s) / dy;
-        const float laplace =
-            (ve1 - 2.0f * vc + vw1) / (dx * dx) + (vn1 - 2.0f * vc + vs1) / (dy * dy);
+        const float convective = sdiv<SP>(f_e - f_w, dx, g.r_dx) + sdiv<SP>(f_n - f_s, dy, g.r_dy);
+        const float laplace = sdiv<SP>(ve1 - 2.0f * vc + vw1, dx * dx, g.r_dxx) +
+                              sdiv<SP>(vn1 - 2.0f * vc + vs1, dy * dy, g.r_dyy);
         r = vc + dt * (-convective + nu * laplace);
     }
-    f.v_star[cv] = r;
+    return r;
+}
+
+template <int SCHEME, int SP>
+__global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float dt_override,
+                                                        int row_lo, int nbx) {
+    const int bid = xcd_block(g);
+    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + bid / nbx;
+    if (i > g.nx - 1) return;
+    const GAcc a{f.u, f.v, (long)lj * (g.nx + 1) + i, (long)lj * g.nx + i, g.nx + 1, g.nx};
+    f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+}
+
+// Both predictors in one pass (piso_step's K1 + K2): each thread computes the
+// u face and the v face at (i, lj), sharing the u / v loads through L1; u rows
+// run to u_hi, v rows to v_hi (v also covers the slab's top face row).  Same
+// values as the two single kernels (one launch and one pass over u, v less).
+// Measured alternatives on the bench workload (r1): 4 columns per thread
+// with strided scalar loads 185 us, an LDS-staged 256 x 16 tile 147 us,
+// this form 113 us.
+template <int SCHEME, int SP>
+__global__ __launch_bounds__(kBlock) void k_predict(Geom g, Fields f, float dt_override, int row_lo,
+                                                    int u_hi, int v_hi, int nbx) {
+    const int bid = xcd_block(g);
+    const int i = 1 + (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int lj = row_lo + bid / nbx;
+    const GAcc a{f.u, f.v, (long)lj * (g.nx + 1) + i, (long)lj * g.nx + i, g.nx + 1, g.nx};
+    if (lj <= u_hi && i <= g.nx)
+        f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+    if (lj <= v_hi && i <= g.nx - 1)
+        f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
 }
 
 // ------------------------------------------------------------ divergence (K3)
 
 // rhs = div(u*, v*) / dt on every owned pressure cell (model.rs:1406-1440).
+// A thread owns 4 consecutive cells: v* rows and the rhs row are 16-byte
+// aligned (pitch nx, nx % 8 == 0) and move as float4; the u* row (pitch nx+1)
+// is read as 5 scalars.  One float per thread capped this stream at ~3 TB/s.
+template <int SP>
 __global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pass,
                                                        float dt_override, int nbx) {
     if (pass_off(f.ctl, pass)) return;
     const int bid = xcd_block(g);
-    const int i = (bid % nbx) * kBlock + (int)threadIdx.x;
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
     const int lj = bid / nbx;
     const int nx = g.nx, W = nx + 1;
-    if (i >= nx) return;
+    if (i0 >= nx) return;
     const float dt = dt_of(f.ctl, dt_override);
-    const float *__restrict__ us = f.u_star;
-    const float *__restrict__ vs = f.v_star;
-    const float u_e = us[(long)lj * W + i + 1];
-    const float u_w = us[(long)lj * W + i];
-    const float v_n = vs[(long)(lj + 1) * nx + i];
-    const float v_s = vs[(long)lj * nx + i];
-    f.rhs[(long)lj * nx + i] = ((u_e - u_w) / g.dx + (v_n - v_s) / g.dy) / dt;
+    const float *__restrict__ us = f.u_star + (long)lj * W + i0;
+    const float4 vs = *reinterpret_cast<const float4 *>(f.v_star + (long)lj * nx + i0);
+    const float4 vn = *reinterpret_cast<const float4 *>(f.v_star + (long)(lj + 1) * nx + i0);
+    const float u0 = us[0], u1 = us[1], u2 = us[2], u3 = us[3], u4 = us[4];
+    const float rdx = g.r_dx, rdy = g.r_dy, dx = g.dx, dy = g.dy;
+    float4 r;
+    r.x = (sdiv<SP>(u1 - u0, dx, rdx) + sdiv<SP>(vn.x - vs.x, dy, rdy)) / dt;
+    r.y = (sdiv<SP>(u2 - u1, dx, rdx) + sdiv<SP>(vn.y - vs.y, dy, rdy)) / dt;
+    r.z = (sdiv<SP>(u3 - u2, dx, rdx) + sdiv<SP>(vn.z - vs.z, dy, rdy)) / dt;
+    r.w = (sdiv<SP>(u4 - u3, dx, rdx) + sdiv<SP>(vn.w - vs.w, dy, rdy)) / dt;
+    *reinterpret_cast<float4 *>(f.rhs + (long)lj * nx + i0) = r;
 }
 
 // ---------------------------------------------------------------- Jacobi (K4)
@@ -484,6 +533,7 @@ __global__ void k_fold_slots(uint32_t *dst, uint32_t *slots, int n) {
 // faces nx-7..nx-1 are the scalar tail and associate (dt * dp) / dx (Q9).
 // v: global rows 1..=ny-1 held by this slab (incl. the shared face row).
 // p += p'.
+template <int SP>
 __global__ __launch_bounds__(kBlock) void k_corrector(Geom g, Fields f, int pass,
                                                       float dt_override, int nbx) {
     Ctl *c = f.ctl;
@@ -501,15 +551,15 @@ __global__ __launch_bounds__(kBlock) void k_corrector(Geom g, Fields f, int pass
         const float p_left = pp[(long)lj * nx + i - 1];
         const long k = (long)lj * W + i;
         if (i >= nx - 7)
-            f.u[k] = f.u_star[k] - dt * (p_right - p_left) / g.dx;
+            f.u[k] = f.u_star[k] - sdiv<SP>(dt * (p_right - p_left), g.dx, g.r_dx);
         else
-            f.u[k] = f.u_star[k] - dt * ((p_right - p_left) / g.dx);
+            f.u[k] = f.u_star[k] - dt * sdiv<SP>(p_right - p_left, g.dx, g.r_dx);
     }
     if (i < nx && j >= 1 && j <= g.ny - 1) {
         const float p_top = pp[(long)lj * nx + i];
         const float p_bottom = pp[(long)(lj - 1) * nx + i];
         const long k = (long)lj * nx + i;
-        f.v[k] = f.v_star[k] - dt * ((p_top - p_bottom) / g.dy);
+        f.v[k] = f.v_star[k] - dt * sdiv<SP>(p_top - p_bottom, g.dy, g.r_dy);
     }
     if (i < nx && lj < g.nyl) {
         const long k = (long)lj * nx + i;
@@ -584,6 +634,7 @@ __global__ __launch_bounds__(1024) void k_boundary(Geom g, Fields f) {
 // touched between step start and here, the value it overwrites IS u_old/v_old:
 // |new - old| needs no copy of the old fields and no second read.  Obstacle
 // faces are bit 1 of the device masks.  Same grid as k_corrector.
+template <int SP>
 __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, float dt_override,
                                                            int nbx) {
     Ctl *c = f.ctl;
@@ -614,13 +665,14 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, flo
                 } else if (i == nx) {
                     // outflow copies the corrected face nx-1 (scalar tail association, Q9)
                     nw = g.bc_kind == 0
-                             ? f.u_star[k - 1] - dt * (pp[rp + nx - 1] - pp[rp + nx - 2]) / g.dx
+                             ? f.u_star[k - 1] - sdiv<SP>(dt * (pp[rp + nx - 1] - pp[rp + nx - 2]),
+                                                          g.dx, g.r_dx)
                              : 0.0f;
                 } else {
                     const float p_right = pp[rp + i];
                     const float p_left = pp[rp + i - 1];
-                    nw = (i >= nx - 7) ? f.u_star[k] - dt * (p_right - p_left) / g.dx
-                                       : f.u_star[k] - dt * ((p_right - p_left) / g.dx);
+                    nw = (i >= nx - 7) ? f.u_star[k] - sdiv<SP>(dt * (p_right - p_left), g.dx, g.r_dx)
+                                       : f.u_star[k] - dt * sdiv<SP>(p_right - p_left, g.dx, g.r_dx);
                 }
                 if (f.n_obs > 0 && (f.mask_u[k] & 2)) nw = 0.0f;
                 const float old = f.u[k];
@@ -636,7 +688,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, flo
                 } else {
                     const float p_top = pp[k];
                     const float p_bottom = pp[k - nx];
-                    nw = f.v_star[k] - dt * ((p_top - p_bottom) / g.dy);
+                    nw = f.v_star[k] - dt * sdiv<SP>(p_top - p_bottom, g.dy, g.r_dy);
                 }
                 if (f.n_obs > 0 && (f.mask_v[k] & 2)) nw = 0.0f;
                 const float old = f.v[k];
@@ -761,12 +813,14 @@ void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipSt
     if (ghi < glo) return;
     const int nbx = cdiv(g.nx, kBlock);
     const dim3 grid(nbx * (ghi - glo + 1));
-    if (g.scheme == 0)
-        hipLaunchKernelGGL(k_u_predictor<0>, grid, dim3(kBlock), 0, s, g, f, dt_override,
-                           glo - g.j0, nbx);
-    else
-        hipLaunchKernelGGL(k_u_predictor<1>, grid, dim3(kBlock), 0, s, g, f, dt_override,
-                           glo - g.j0, nbx);
+#define CFD_LAUNCH_U(SC, SPV) hipLaunchKernelGGL((k_u_predictor<SC, SPV>), grid, dim3(kBlock), 0, s, \
+                                                 g, f, dt_override, glo - g.j0, nbx)
+    if (g.scheme == 0) {
+        if (g.sp_pow2) CFD_LAUNCH_U(0, 1); else CFD_LAUNCH_U(0, 0);
+    } else {
+        if (g.sp_pow2) CFD_LAUNCH_U(1, 1); else CFD_LAUNCH_U(1, 0);
+    }
+#undef CFD_LAUNCH_U
 }
 
 void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
@@ -775,19 +829,43 @@ void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipSt
     if (ghi < glo) return;
     const int nbx = cdiv(g.nx - 1, kBlock);
     const dim3 grid(nbx * (ghi - glo + 1));
-    if (g.scheme == 0)
-        hipLaunchKernelGGL(k_v_predictor<0>, grid, dim3(kBlock), 0, s, g, f, dt_override,
-                           glo - g.j0, nbx);
-    else
-        hipLaunchKernelGGL(k_v_predictor<1>, grid, dim3(kBlock), 0, s, g, f, dt_override,
-                           glo - g.j0, nbx);
+#define CFD_LAUNCH_V(SC, SPV) hipLaunchKernelGGL((k_v_predictor<SC, SPV>), grid, dim3(kBlock), 0, s, \
+                                                 g, f, dt_override, glo - g.j0, nbx)
+    if (g.scheme == 0) {
+        if (g.sp_pow2) CFD_LAUNCH_V(0, 1); else CFD_LAUNCH_V(0, 0);
+    } else {
+        if (g.sp_pow2) CFD_LAUNCH_V(1, 1); else CFD_LAUNCH_V(1, 0);
+    }
+#undef CFD_LAUNCH_V
+}
+
+void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+    const int glo = g.j0 > 1 ? g.j0 : 1;
+    const int u_hi = (g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2);
+    const int v_hi = (g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1);
+    const int ghi = u_hi > v_hi ? u_hi : v_hi;
+    if (ghi < glo) return;
+    const int nbx = cdiv(g.nx, kBlock);
+    const dim3 grid(nbx * (ghi - glo + 1));
+#define CFD_LAUNCH_P(SC, SPV) hipLaunchKernelGGL((k_predict<SC, SPV>), grid, dim3(kBlock), 0, s, g, f, \
+                                                 dt_override, glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx)
+    if (g.scheme == 0) {
+        if (g.sp_pow2) CFD_LAUNCH_P(0, 1); else CFD_LAUNCH_P(0, 0);
+    } else {
+        if (g.sp_pow2) CFD_LAUNCH_P(1, 1); else CFD_LAUNCH_P(1, 0);
+    }
+#undef CFD_LAUNCH_P
 }
 
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s) {
-    const int nbx = cdiv(g.nx, kBlock);
-    hipLaunchKernelGGL(k_divergence, dim3(nbx * g.nyl), dim3(kBlock), 0, s, g, f, pass,
-                       dt_override, nbx);
+    const int nbx = cdiv(g.nx / 4, kBlock);
+    if (g.sp_pow2)
+        hipLaunchKernelGGL(k_divergence<1>, dim3(nbx * g.nyl), dim3(kBlock), 0, s, g, f, pass,
+                           dt_override, nbx);
+    else
+        hipLaunchKernelGGL(k_divergence<0>, dim3(nbx * g.nyl), dim3(kBlock), 0, s, g, f, pass,
+                           dt_override, nbx);
 }
 
 void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int row_lo,
@@ -839,15 +917,22 @@ void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, 
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s) {
     const int nbx = cdiv(g.nx + 1, kBlock);
-    hipLaunchKernelGGL(k_corrector, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,
-                       dt_override, nbx);
+    if (g.sp_pow2)
+        hipLaunchKernelGGL(k_corrector<1>, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,
+                           dt_override, nbx);
+    else
+        hipLaunchKernelGGL(k_corrector<0>, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,
+                           dt_override, nbx);
 }
 
 void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
     const int nbx = cdiv(g.nx + 1, kBlock);
     const long ntiles = (long)nbx * (g.nyl + 1);
     const int blocks = (int)std::min<long>(ntiles, 8L * g.n_cu);
-    hipLaunchKernelGGL(k_correct_finish, dim3(blocks), dim3(kBlock), 0, s, g, f, dt_override, nbx);
+    if (g.sp_pow2)
+        hipLaunchKernelGGL(k_correct_finish<1>, dim3(blocks), dim3(kBlock), 0, s, g, f, dt_override, nbx);
+    else
+        hipLaunchKernelGGL(k_correct_finish<0>, dim3(blocks), dim3(kBlock), 0, s, g, f, dt_override, nbx);
 }
 
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s) {

@@ -519,8 +519,7 @@ struct cfd_model {
     // finish = inside update() with no extra corrector passes: the corrector,
     // the boundaries and the step reductions run as one fused pass.
     int enqueue_piso(float dt_override, bool finish = false) {
-        launch_u_predictor(g, f, dt_override, stream);
-        launch_v_predictor(g, f, dt_override, stream);
+        launch_predict(g, f, dt_override, stream);
         if (finish) {
             launch_divergence(g, f, host_driven() ? -1 : 0, dt_override, stream);
             int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
@@ -742,6 +741,21 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     g.r_dx_sq = 1.0f / g.dx_sq;
     g.r_dy_sq = 1.0f / g.dy_sq;
     g.r_denom = 1.0f / g.denom;
+    {
+        // spacings that are exact powers of two: division == reciprocal multiply
+        auto pow2f = [](float c) {
+            int e;
+            return c > 0.0f && std::isfinite(c) && std::frexp(c, &e) == 0.5f &&
+                   std::isnormal(1.0f / c);
+        };
+        g.r_dx = 1.0f / g.dx;
+        g.r_dy = 1.0f / g.dy;
+        g.r_dxx = 1.0f / (g.dx * g.dx);
+        g.r_dyy = 1.0f / (g.dy * g.dy);
+        g.sp_pow2 = pow2f(g.dx) && pow2f(g.dy) && pow2f(g.dx * g.dx) && pow2f(g.dy * g.dy) ? 1 : 0;
+        if (const char *e = getenv("CFD_FASTDIV"))
+            if (atoi(e) == 0) g.sp_pow2 = 0;
+    }
     {
         int rc0 = choose_division(m->stream, g);
         if (rc0) return rc0;
