@@ -51,13 +51,29 @@ def cpu_info():
     return model, os.cpu_count()
 
 
-def cpu_baseline(nx, ny, iters, re, budget_s, state):
-    """The oracle (scalar/auto-vectorised C restatement, 1 thread, like the
-    reference's single worker thread model.rs:1287) on the same workload,
+def cpu_threads():
+    """Host threads this job may use: the box's CPU share (OMP_NUM_THREADS is
+    set to it on the GPU box), else the affinity mask, capped at 16."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return 1
+
+
+def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=3):
+    """The oracle (scalar/auto-vectorised C restatement) on the same workload,
     started from the GPU model's final state (so it sweeps the same developed,
-    mostly non-zero fields, subnormals included, as the reference would)."""
+    mostly non-zero fields, subnormals included, as the reference would).
+    threads=1 is the reference's single worker thread (model.rs:1287);
+    threads>1 splits the row loops over OpenMP threads, bit-identical results
+    (oracle/cfd_oracle.h orc_set_threads)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
     from oracle import OracleModel
+    orc.set_threads(threads)
     m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
                     jacobi_iters=iters, corrector_passes=0, tol_enabled=0)
     for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
@@ -71,15 +87,19 @@ def cpu_baseline(nx, ny, iters, re, budget_s, state):
         m.update()
         steps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or steps >= 3:
+        if el >= budget_s or steps >= max_steps:
             break
+    orc.set_threads(1)
     model, ncpu = cpu_info()
-    return {"value": nx * ny * iters * steps / el, "unit": "cell-updates/s", "cores": 1,
+    return {"value": nx * ny * iters * steps / el, "unit": "cell-updates/s", "cores": threads,
             "kind": "port",
             "sample": f"{steps} full update() step(s) of the same {nx}x{ny} cavity "
                       f"({iters} sweeps/step) from the GPU run's final state (step "
                       f"{state['simulation_step']}) after 1 warm-up step, oracle/cfd_oracle.c, "
-                      f"1 thread; ms/step {1e3 * el / steps:.0f}; host {model}, {ncpu} cpus"}
+                      f"{threads} thread(s)"
+                      + (" (the reference's single worker thread)" if threads == 1 else
+                         " (OpenMP row split, same bits)")
+                      + f"; ms/step {1e3 * el / steps:.0f}; host {model}, {ncpu} cpus"}
 
 
 def pmc_traffic(kernel, slab):
@@ -241,6 +261,12 @@ def main():
         }
         if n == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(nx, ny, args.iters, args.re, args.cpu_budget, state)
+            nt = cpu_threads()
+            if nt > 1:
+                # the same restatement over all of this job's host cores
+                out["cpu_baseline_multicore"] = cpu_baseline(
+                    nx, ny, args.iters, args.re, args.cpu_budget / 2, state, threads=nt,
+                    max_steps=20)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -26,8 +26,23 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define LANES 8 /* model.rs:11 */
+
+/* Row-loop threads (orc_set_threads); 1 = the reference's single thread. */
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+int orc_get_threads(void) { return g_threads; }
+static inline int thread_id(void) {
+#ifdef _OPENMP
+    return omp_get_thread_num();
+#else
+    return 0;
+#endif
+}
 
 struct orc_model {
     size_t nx, ny;
@@ -267,6 +282,7 @@ static inline void compute_ustar_1(orc_model *m, float dt_sub, size_t i, size_t 
  * (1..nx).step_by(8) -> with nx % 8 == 0 the lanes cover faces 1..=nx. */
 void orc_u_predictor(orc_model *m, float dt_sub) {
     size_t nx = m->nx, ny = m->ny;
+#pragma omp parallel for schedule(static) num_threads(g_threads)
     for (size_t j = 1; j < ny - 1; ++j) {
         for (size_t i = 1; i < nx; i += LANES) {
             for (size_t k = 0; k < LANES; ++k) {
@@ -407,6 +423,7 @@ static inline void compute_vstar_1(orc_model *m, float dt_sub, size_t i, size_t 
 void orc_v_predictor(orc_model *m, float dt_sub) {
     size_t nx = m->nx, ny = m->ny;
     const float *u = U_(m);
+#pragma omp parallel for schedule(static) num_threads(g_threads)
     for (size_t j = 1; j < ny; ++j) {
         for (size_t i = 1; i < nx - 1; i += LANES) {
             int last = (i + LANES > nx - 1);
@@ -444,6 +461,7 @@ void orc_divergence(orc_model *m, float dt_sub) {
     const float *us = m->f[ORC_U_STAR], *vs = m->f[ORC_V_STAR];
     float *rhs = m->f[ORC_RHS];
     float dx = m->dx, dy = m->dy;
+#pragma omp parallel for schedule(static) num_threads(g_threads)
     for (size_t j = 0; j < ny; ++j) {
         for (size_t i = 0; i < nx; ++i) {
             float u_e = us[(i + 1) + j * (nx + 1)];
@@ -491,25 +509,36 @@ float orc_jacobi_pressure(orc_model *m) {
     /* columns covered by full 8-lane chunks: i in [1, simd_end) */
     size_t simd_end = 1;
     while (simd_end + LANES <= nx - 1) simd_end += LANES;
-    /* per-column running maxima (element-wise, so the row loop vectorises) */
-    float *colmax = (float *)malloc((nx + 8) * sizeof(float));
+    /* per-column running maxima (element-wise, so the row loop vectorises),
+     * one set per thread; the max over all of them is order-independent */
+    const int nt = g_threads;
+    const size_t cstride = nx + 8;
+    float *colmax = (float *)malloc((size_t)nt * cstride * sizeof(float));
     for (int iter = 0; iter < m->jacobi_iters; ++iter) {
         const float *pp = m->f[ORC_PP];
         float *ppn = m->f[ORC_PPN];
-        for (size_t i = 0; i < nx; ++i) colmax[i] = 0.0f;
-        for (size_t j = 1; j < ny - 1; ++j) {
-            const size_t row = j * nx;
-            for (size_t i = 1; i < simd_end; ++i) {
-                float nv = jac_point(pp, rhs, row + i, nx, dx_sq, dy_sq, denom, jacobi_omega, om1);
-                ppn[row + i] = nv;
-                float e = fabsf(nv - pp[row + i]);
-                colmax[i] = e > colmax[i] ? e : colmax[i];
+#pragma omp parallel num_threads(nt)
+        {
+            float *cm = colmax + (size_t)thread_id() * cstride;
+            for (size_t i = 0; i < nx; ++i) cm[i] = 0.0f;
+#pragma omp for schedule(static)
+            for (size_t j = 1; j < ny - 1; ++j) {
+                const size_t row = j * nx;
+                for (size_t i = 1; i < simd_end; ++i) {
+                    float nv = jac_point(pp, rhs, row + i, nx, dx_sq, dy_sq, denom, jacobi_omega, om1);
+                    ppn[row + i] = nv;
+                    float e = fabsf(nv - pp[row + i]);
+                    cm[i] = e > cm[i] ? e : cm[i];
+                }
+                for (size_t i = simd_end; i < nx; ++i)   /* scalar tail, no residual */
+                    ppn[row + i] = jac_point(pp, rhs, row + i, nx, dx_sq, dy_sq, denom, jacobi_omega, om1);
             }
-            for (size_t i = simd_end; i < nx; ++i)   /* scalar tail, no residual */
-                ppn[row + i] = jac_point(pp, rhs, row + i, nx, dx_sq, dy_sq, denom, jacobi_omega, om1);
         }
         max_error = 0.0f;
-        for (size_t i = 1; i < simd_end; ++i) max_error = colmax[i] > max_error ? colmax[i] : max_error;
+        for (int t = 0; t < nt; ++t) {
+            const float *cm = colmax + (size_t)t * cstride;
+            for (size_t i = 1; i < simd_end; ++i) max_error = cm[i] > max_error ? cm[i] : max_error;
+        }
         /* std::mem::swap (model.rs:805) */
         float *tmp = m->f[ORC_PP];
         m->f[ORC_PP] = m->f[ORC_PPN];
@@ -540,6 +569,7 @@ void orc_corrector(orc_model *m, float dt_sub) {
     float dx = m->dx, dy = m->dy;
     float *u = U_(m), *v = V_(m), *p = m->f[ORC_P];
     const float *us = m->f[ORC_U_STAR], *vs = m->f[ORC_V_STAR], *pp = m->f[ORC_PP];
+#pragma omp parallel for schedule(static) num_threads(g_threads)
     for (size_t j = 0; j < ny; ++j) {
         for (size_t i = 1; i < nx; i += LANES) {
             if (i + LANES > nx) {
@@ -562,6 +592,7 @@ void orc_corrector(orc_model *m, float dt_sub) {
             }
         }
     }
+#pragma omp parallel for schedule(static) num_threads(g_threads)
     for (size_t j = 1; j < ny; ++j) {
         for (size_t i = 0; i < nx; i += LANES) {
             size_t nl = (i + LANES > nx) ? (nx - i) : LANES;
@@ -578,6 +609,7 @@ void orc_corrector(orc_model *m, float dt_sub) {
             }
         }
     }
+#pragma omp parallel for schedule(static) num_threads(g_threads)
     for (size_t k = 0; k < nx * ny; ++k) p[k] += pp[k];
 }
 
@@ -635,7 +667,10 @@ void orc_boundary_conditions(orc_model *m) {
 /* compute_automatic_time_step (model.rs:877-889). */
 float orc_auto_dt(const orc_model *m) {
     float max_u = 0.0f, max_v = 0.0f;
+    /* maxima over NaN-free values are order-independent: threads are exact */
+#pragma omp parallel for schedule(static) num_threads(g_threads) reduction(max : max_u)
     for (size_t k = 0; k < m->len[ORC_U]; ++k) max_u = fmaxf(max_u, fabsf(U_(m)[k]));
+#pragma omp parallel for schedule(static) num_threads(g_threads) reduction(max : max_v)
     for (size_t k = 0; k < m->len[ORC_V]; ++k) max_v = fmaxf(max_v, fabsf(V_(m)[k]));
     float max_vel = fmaxf(max_u, max_v);
     if (max_vel == 0.0f) return m->dt;
@@ -696,8 +731,10 @@ void orc_update(orc_model *m) {
     float dt_sub = m->dt / 1.0f; /* substep_count = 1 (model.rs:267, 317) */
     orc_piso_step(m, dt_sub);
     float ru = 0.0f, rv = 0.0f;
+#pragma omp parallel for schedule(static) num_threads(g_threads) reduction(max : ru)
     for (size_t k = 0; k < m->len[ORC_U]; ++k)
         ru = fmaxf(ru, fabsf(U_(m)[k] - m->f[ORC_U_OLD][k]));
+#pragma omp parallel for schedule(static) num_threads(g_threads) reduction(max : rv)
     for (size_t k = 0; k < m->len[ORC_V]; ++k)
         rv = fmaxf(rv, fabsf(V_(m)[k] - m->f[ORC_V_OLD][k]));
     m->last_u_residual = ru;

@@ -82,6 +82,14 @@ void orc_mg_prolongate(const float *coarse, int nx_c, int ny_c, float *fine, int
 void orc_mg_vcycle(float *p, const float *rhs, int nx, int ny, double dx, double dy);
 float orc_mg_residual(const float *p, const float *rhs, int nx, int ny, double dx, double dy);
 
+/* Threads for the row loops of the Model::update path (default 1, the
+ * reference's single worker thread, model.rs:1287).  n > 1 is the labelled
+ * all-core CPU baseline of SURVEY §8(d): rows split across OpenMP threads,
+ * per-thread maxima folded afterwards; every result is bit-identical to the
+ * 1-thread run (no sums change order, maxima are order-independent). */
+void orc_set_threads(int n);
+int orc_get_threads(void);
+
 /* Raw field access. Field ids: */
 enum { ORC_U = 0, ORC_V, ORC_P, ORC_U_OLD, ORC_V_OLD, ORC_U_STAR, ORC_V_STAR,
        ORC_RHS, ORC_PP, ORC_PPN, ORC_NFIELDS };

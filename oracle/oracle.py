@@ -87,8 +87,21 @@ def lib():
         L.orc_mg_vcycle.argtypes = [FP, FP, i32, i32, f64, f64]
         L.orc_mg_residual.argtypes = [FP, FP, i32, i32, f64, f64]
         L.orc_mg_residual.restype = C.c_float
+        L.orc_set_threads.argtypes = [i32]
+        L.orc_get_threads.restype = i32
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """Row-loop threads of the Model::update restatement (1 = the reference's
+    single worker thread, model.rs:1287; >1 = the labelled all-core baseline,
+    bit-identical results)."""
+    lib().orc_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return int(lib().orc_get_threads())
 
 
 def make_params(dt=0.005, viscosity=1e-6, target_inlet_velocity=1.0, scheme=0, inlet_profile=0,
