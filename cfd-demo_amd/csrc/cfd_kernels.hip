@@ -100,7 +100,6 @@ __device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, floa
                                             int i, int lj, const A &a) {
     const int nx = g.nx, ny = g.ny, W = nx + 1;
     const int j = g.j0 + lj;
-    const long c = (long)lj * W + i;
     const float uc = a.U(0, 0), ue1 = a.U(1, 0), uw1 = a.U(-1, 0), un1 = a.U(0, 1), us1 = a.U(0, -1);
     const float vn = a.V(0, 1), vs = a.V(0, 0);
     float ue, uw, un, us;
@@ -276,6 +275,98 @@ __global__ __launch_bounds__(kBlock) void k_predict(Geom g, Fields f, float dt_o
         f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
     if (lj <= v_hi && i <= g.nx - 1)
         f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+}
+
+// Register-backed stencil for k_predict4: u rows lj-1..lj+1 and v rows
+// lj-1..lj+1 at columns i0-1..i0+4, column q of the thread's four.  Every
+// (di, dj) the first-order helpers ask for is a compile-time index once the
+// column loop is unrolled, so the values never leave registers.
+struct RAcc {
+    const float (&ur)[3][6];
+    const float (&vr)[3][6];
+    int q;
+    __device__ __forceinline__ float U(int di, int dj) const { return ur[dj + 1][q + 1 + di]; }
+    __device__ __forceinline__ float V(int di, int dj) const { return vr[dj + 1][q + 1 + di]; }
+};
+
+// Both first-order predictors with four columns per thread (i0 = 4t): the
+// pitch-nx v rows move as float4 (v row lj-1, lj, lj+1 and the v* store), the
+// pitch-(nx+1) u rows as scalars, and each value is loaded once for the eight
+// faces it feeds (u_pred_val / v_pred_val over an RAcc, so the arithmetic is
+// the single-face kernel's, bit for bit).  Face 0 and column 0 are not
+// predicted (model.rs:538, :586); the thread owning columns nx-4..nx-1 also
+// predicts u face nx, through the flat-indexed GAcc (its east and north
+// neighbours wrap to the next row, Q1-Q3).  Requires 16-byte aligned v and
+// v* rows (checked by the launcher).
+template <int SP>
+__global__ __launch_bounds__(kBlock) void k_predict4(Geom g, Fields f, float dt_override,
+                                                     int row_lo, int u_hi, int v_hi, int nbx) {
+    const int bid = xcd_block(g);
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
+    const int lj = row_lo + bid / nbx;
+    const int nx = g.nx, W = nx + 1;
+    if (i0 >= nx) return;
+    const float *__restrict__ u = f.u;
+    const float *__restrict__ v = f.v;
+    const long ku = (long)lj * W + i0, kv = (long)lj * nx + i0;
+    const bool do_u = lj <= u_hi, do_v = lj <= v_hi;
+    float ur[3][6], vr[3][6];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) ur[r][c] = vr[r][c] = 0.0f;
+    // shared by both predictors: u row lj (cols i0-1..i0+4), v rows lj, lj+1
+    ur[1][0] = i0 > 0 ? u[ku - 1] : 0.0f;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) ur[1][c + 1] = u[ku + c];
+    {
+        const float4 a = *reinterpret_cast<const float4 *>(v + kv);
+        const float4 b = *reinterpret_cast<const float4 *>(v + kv + nx);
+        vr[1][1] = a.x; vr[1][2] = a.y; vr[1][3] = a.z; vr[1][4] = a.w;
+        vr[2][1] = b.x; vr[2][2] = b.y; vr[2][3] = b.z; vr[2][4] = b.w;
+    }
+    if (do_u) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            ur[0][c + 1] = u[ku - W + c];
+            ur[2][c + 1] = u[ku + W + c];
+        }
+    }
+    if (do_v) {
+        const float4 a = *reinterpret_cast<const float4 *>(v + kv - nx);
+        vr[0][1] = a.x; vr[0][2] = a.y; vr[0][3] = a.z; vr[0][4] = a.w;
+        vr[1][0] = i0 > 0 ? v[kv - 1] : 0.0f;
+        vr[1][5] = v[kv + 4];   // column nx wraps to the next row's column 0 (flat index)
+    }
+    if (do_u) {
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            o[q] = u_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAcc{ur, vr, q});
+        float *__restrict__ us = f.u_star + ku;
+        if (i0 > 0) us[0] = o[0];
+        us[1] = o[1];
+        us[2] = o[2];
+        us[3] = o[3];
+        if (i0 + 4 == nx) {
+            const GAcc a{f.u, f.v, ku + 4, kv + 4, W, nx};
+            us[4] = u_pred_val<0, SP>(g, f, dt_override, nx, lj, a);
+        }
+    }
+    if (do_v) {
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            o[q] = v_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAcc{ur, vr, q});
+        float *__restrict__ vs = f.v_star + kv;
+        if (i0 > 0) {
+            *reinterpret_cast<float4 *>(vs) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+            vs[1] = o[1];
+            vs[2] = o[2];
+            vs[3] = o[3];
+        }
+    }
 }
 
 // ------------------------------------------------------------ divergence (K3)
@@ -970,6 +1061,22 @@ void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream
     const int v_hi = (g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1);
     const int ghi = u_hi > v_hi ? u_hi : v_hi;
     if (ghi < glo) return;
+    static const int vec = [] {
+        const char *e = getenv("CFD_PRED_VEC");
+        return e ? atoi(e) : 1;
+    }();
+    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    if (vec && g.scheme == 0 && g.nx % 4 == 0 && a16(f.v) && a16(f.v_star)) {
+        const int nbx4 = cdiv(g.nx / 4, kBlock);
+        const dim3 grid4(nbx4 * (ghi - glo + 1));
+        if (g.sp_pow2)
+            hipLaunchKernelGGL(k_predict4<1>, grid4, dim3(kBlock), 0, s, g, f, dt_override,
+                               glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx4);
+        else
+            hipLaunchKernelGGL(k_predict4<0>, grid4, dim3(kBlock), 0, s, g, f, dt_override,
+                               glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx4);
+        return;
+    }
     const int nbx = cdiv(g.nx, kBlock);
     const dim3 grid(nbx * (ghi - glo + 1));
 #define CFD_LAUNCH_P(SC, SPV) hipLaunchKernelGGL((k_predict<SC, SPV>), grid, dim3(kBlock), 0, s, g, f, \
