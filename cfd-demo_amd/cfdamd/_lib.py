@@ -8,7 +8,8 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(ROOT, "lib", "libcfd_amd.so")
+# CFD_LIB: an alternative build of the same library (tools/build_variants.sh, tuning only)
+LIB_PATH = os.environ.get("CFD_LIB") or os.path.join(ROOT, "lib", "libcfd_amd.so")
 
 # Every entry point include/cfd.h declares (checked by tests/test_abi.py).
 EXPORTS = [

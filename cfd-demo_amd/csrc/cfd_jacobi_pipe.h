@@ -29,12 +29,37 @@ constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 constexpr int clcm(int a, int b) { return a / cgcd(a, b) * b; }
 constexpr int kFarOffset = 0x7FFF0000;   // voffset of a lane that must not touch memory
 
+// cache-policy bits of the march's buffer instructions (gfx950 CPol: 1 SC0,
+// 2 NT, 16 SC1): p' input loads, rhs loads, p'_new stores
+#ifndef CFD_CPOL_PLD
+#define CFD_CPOL_PLD 0
+#endif
+#ifndef CFD_CPOL_RLD
+#define CFD_CPOL_RLD 0
+#endif
+#ifndef CFD_CPOL_ST
+#define CFD_CPOL_ST 0
+#endif
+// CFD_TRIM 1: skip the prefetches past the segment's last input row (they
+// would fetch rows the neighbouring segment owns); CFD_PIPE_WAVES: waves per
+// workgroup; CFD_PD4: prefetch distance at T = 4
+#ifndef CFD_TRIM
+#define CFD_TRIM 1
+#endif
+#ifndef CFD_PIPE_WAVES
+#define CFD_PIPE_WAVES kJacWavesPerBlock
+#endif
+#ifndef CFD_PD4
+#define CFD_PD4 2
+#endif
+constexpr int kPipeWaves = CFD_PIPE_WAVES;
+
 // prefetch distance per T: deep enough to cover HBM latency with a short
 // unroll period U = lcm(3, PD, T+PD)
 template <int T> struct PipeDepth { static constexpr int PD = 4; };   // T 2: U 12; T 8: U 12
 template <> struct PipeDepth<1> { static constexpr int PD = 2; };     // U 6
 template <> struct PipeDepth<3> { static constexpr int PD = 3; };     // U 6
-template <> struct PipeDepth<4> { static constexpr int PD = 2; };     // U 6
+template <> struct PipeDepth<4> { static constexpr int PD = CFD_PD4; };  // PD 2: U 6
 template <> struct PipeDepth<5> { static constexpr int PD = 3; };     // U 24
 template <> struct PipeDepth<6> { static constexpr int PD = 3; };     // U 9
 template <> struct PipeDepth<7> { static constexpr int PD = 2; };     // U 18
@@ -63,8 +88,9 @@ template <int VEC> struct Lane;
 
 template <> struct Lane<4> {
     using V = float4;
+    template <int CP>
     static __device__ __forceinline__ V load(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, CP);
         return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                            __uint_as_float(v.w));
     }
@@ -72,7 +98,7 @@ template <> struct Lane<4> {
                                                  int so) {
         const u32x4 v = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z),
                          __float_as_uint(x.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, vo, so, CFD_CPOL_ST);
     }
     template <int FAST>
     static __device__ __forceinline__ V row(const V &B, const V &C, const V &T, const V &Rh,
@@ -101,14 +127,15 @@ template <> struct Lane<4> {
 
 template <> struct Lane<2> {
     using V = float2;
+    template <int CP>
     static __device__ __forceinline__ V load(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, CP);
         return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
     }
     static __device__ __forceinline__ void store(const V &x, __amdgpu_buffer_rsrc_t rs, int vo,
                                                  int so) {
         const u32x2 v = {__float_as_uint(x.x), __float_as_uint(x.y)};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, so, CFD_CPOL_ST);
     }
     template <int FAST>
     static __device__ __forceinline__ V row(const V &B, const V &C, const V &T, const V &Rh,
@@ -153,10 +180,12 @@ struct Pipe {
 
     __device__ __forceinline__ int act(int row) const { return abase + dir * row; }
 
+    template <int CP>
     __device__ __forceinline__ V ld(__amdgpu_buffer_rsrc_t rs, int vrow) const {
         const int row = act(vrow);
-        const bool ok = row >= -hg && row < nyl + hg;   // uniform: scalar descriptor select
-        return L::load(ok ? rs : rs_null, vo_ld, ok ? (row + hg) * row_bytes : 0);
+        // uniform: scalar descriptor select
+        const bool ok = row >= -hg && row < nyl + hg && (!CFD_TRIM || vrow < k_first + S);
+        return L::template load<CP>(ok ? rs : rs_null, vo_ld, ok ? (row + hg) * row_bytes : 0);
     }
     __device__ __forceinline__ void st(const V &x, int row) const {
         L::store(x, rs_d, vo_st, (row + hg) * row_bytes);
@@ -180,7 +209,7 @@ struct Pipe {
         if (GUARD == 2 && v >= S) return;
         const int k = k_first + v;
         W[0][V_ % 3] = PQ[V_ % PD];                             // input row k
-        PQ[V_ % PD] = ld(rs_p, k + PD);
+        PQ[V_ % PD] = ld<CFD_CPOL_PLD>(rs_p, k + PD);
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
             if (GUARD == 0 && V_ < 2 * s) continue;              // compile-time
@@ -202,7 +231,7 @@ struct Pipe {
                 if (EDGE && r == g_last) st(n, g_top);
             }
         }
-        RH[(V_ - 1 + PD + NR) % NR] = ld(rs_r, k - 1 + PD);     // rhs row k-1+PD
+        RH[(V_ - 1 + PD + NR) % NR] = ld<CFD_CPOL_RLD>(rs_r, k - 1 + PD);     // rhs row k-1+PD
     }
 
     template <int V_, bool EDGE>
@@ -232,7 +261,7 @@ struct Pipe {
 };
 
 template <int T, int FAST, int VEC>
-__global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_pipe(
+__global__ __launch_bounds__(kPipeWaves * 64) void k_jacobi_pipe(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int it, int par, int out_lo, int out_hi, int nwc,
     int nseg) {
@@ -246,7 +275,7 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_pipe(
     const int lane = (int)threadIdx.x & 63;
     const int bid = xcd_block(g);
     const int wc = bid % nwc;
-    const int seg = (bid / nwc) * kJacWavesPerBlock + wave;
+    const int seg = (bid / nwc) * kPipeWaves + wave;
     const int nrows = out_hi - out_lo;
     if (seg >= nseg) return;
     // balanced segments: nseg row ranges differing by at most one row
@@ -316,16 +345,16 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi_pipe(
     }
     // prologue: p' rows k_first .. k_first+PD-1, rhs rows k_first .. k_first+PD-2
 #pragma unroll
-    for (int q = 0; q < Wv::PD; ++q) w.PQ[q] = w.ld(w.rs_p, w.k_first + q);
+    for (int q = 0; q < Wv::PD; ++q) w.PQ[q] = w.template ld<CFD_CPOL_PLD>(w.rs_p, w.k_first + q);
 #pragma unroll
-    for (int q = 0; q < Wv::NR; ++q) w.RH[q] = q < Wv::PD - 1 ? w.ld(w.rs_r, w.k_first + q) : z;
+    for (int q = 0; q < Wv::NR; ++q) w.RH[q] = q < Wv::PD - 1 ? w.template ld<CFD_CPOL_RLD>(w.rs_r, w.k_first + q) : z;
     if (edge)
         w.template run<true>();
     else
         w.template run<false>();
     if (!res_slots) return;
     const float m = wave_max(out_lane ? w.m : 0.0f);
-    if (lane == 0) publish_max(res_slots, bid * kJacWavesPerBlock + wave, m);
+    if (lane == 0) publish_max(res_slots, bid * kPipeWaves + wave, m);
 }
 
 template <int VEC, int T>
@@ -338,11 +367,11 @@ void launch_pipe_t(const Geom &g, const Fields &f, int pass, int it, int par, in
         nseg = cdiv(out_hi - out_lo, g.tb_rows);
     } else {
         const int blocks_per_strip = cdiv((long)g.tb_bpc * g.n_cu, nwc);
-        nseg = blocks_per_strip * kJacWavesPerBlock;
+        nseg = blocks_per_strip * kPipeWaves;
         const int max_seg = (out_hi - out_lo) / 8;     // keep >= 8 rows per segment
         if (nseg > max_seg) nseg = std::max(1, max_seg);
     }
-    const dim3 grid(nwc * cdiv(nseg, kJacWavesPerBlock)), block(kJacWavesPerBlock * 64);
+    const dim3 grid(nwc * cdiv(nseg, kPipeWaves)), block(kPipeWaves * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     if (g.fastdiv == 1)
         hipLaunchKernelGGL((k_jacobi_pipe<T, 1, VEC>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl,

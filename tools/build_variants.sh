@@ -1,0 +1,22 @@
+#!/bin/bash
+# Builds variants of libcfd_amd.so that differ only in compile-time knobs of
+# the pipelined Jacobi march (cache-policy bits), for A/B runs on the GPU:
+#   CFD_LIB=cfd-demo_amd/lib/variants/<name>/libcfd_amd.so python tools/tb_one.py
+# Usage: tools/build_variants.sh name:"-DFLAG=1 -DOTHER=2" ...
+set -e
+cd "$(dirname "$0")/../cfd-demo_amd"
+make -s
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt"
+OTHERS=$(ls build/*.o | grep -v cfd_jacobi_pipe2.o)
+for spec in "$@"; do
+  name=${spec%%:*}; defs=${spec#*:}
+  mkdir -p lib/variants/$name
+  /opt/rocm/bin/hipcc $FLAGS $defs -c csrc/cfd_jacobi_pipe2.hip -o lib/variants/$name/pipe2.o &
+done
+wait
+for spec in "$@"; do
+  name=${spec%%:*}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/variants/$name/libcfd_amd.so $OTHERS \
+    lib/variants/$name/pipe2.o -lrccl -lpthread -Wl,-rpath,/opt/rocm/lib
+  rm lib/variants/$name/pipe2.o
+done
