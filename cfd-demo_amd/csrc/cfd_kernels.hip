@@ -369,6 +369,83 @@ __global__ __launch_bounds__(kBlock) void k_predict4(Geom g, Fields f, float dt_
     }
 }
 
+// k_predict4 over RPT consecutive rows per thread: the window of u and v rows
+// lj-1 .. lj+RPT is loaded up front (every load in flight at once, and the
+// rows shared by neighbouring output rows loaded once), then the 8 x RPT
+// faces are computed with the same u_pred_val / v_pred_val arithmetic.
+// Rows past the last row a predictor needs are clamped to it (their values
+// are never used), so no load leaves the allocation.
+struct RAccN {
+    const float (*ur)[6];
+    const float (*vr)[6];
+    int q;
+    __device__ __forceinline__ float U(int di, int dj) const { return ur[dj + 1][q + 1 + di]; }
+    __device__ __forceinline__ float V(int di, int dj) const { return vr[dj + 1][q + 1 + di]; }
+};
+
+template <int SP, int RPT>
+__global__ __launch_bounds__(kBlock) void k_predict4r(Geom g, Fields f, float dt_override,
+                                                      int row_lo, int u_hi, int v_hi, int nbx) {
+    const int bid = xcd_block(g);
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
+    const int lj0 = row_lo + (bid / nbx) * RPT;
+    const int nx = g.nx, W = nx + 1;
+    if (i0 >= nx) return;
+    const float *__restrict__ u = f.u;
+    const float *__restrict__ v = f.v;
+    const int u_cap = u_hi + 1 > v_hi ? u_hi + 1 : v_hi;   // last u row any face reads
+    const int v_cap = v_hi + 1;                            // last v row any face reads
+    float ur[RPT + 2][6], vr[RPT + 2][6];
+#pragma unroll
+    for (int r = 0; r < RPT + 2; ++r) {
+        const int ru = min(lj0 - 1 + r, u_cap), rv = min(lj0 - 1 + r, v_cap);
+        const long ku = (long)ru * W + i0, kv = (long)rv * nx + i0;
+        const bool mid = r >= 1 && r <= RPT;   // output rows: their east/west neighbours too
+        ur[r][0] = (mid && i0 > 0) ? u[ku - 1] : 0.0f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ur[r][c + 1] = u[ku + c];
+        ur[r][5] = mid ? u[ku + 4] : 0.0f;
+        const float4 a = *reinterpret_cast<const float4 *>(v + kv);
+        vr[r][1] = a.x; vr[r][2] = a.y; vr[r][3] = a.z; vr[r][4] = a.w;
+        vr[r][0] = (mid && i0 > 0) ? v[kv - 1] : 0.0f;
+        vr[r][5] = mid ? v[kv + 4] : 0.0f;   // column nx wraps to the next row's column 0
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int lj = lj0 + r;
+        const long ku = (long)lj * W + i0, kv = (long)lj * nx + i0;
+        if (lj <= u_hi) {
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                o[q] = u_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAccN{ur + r, vr + r, q});
+            float *__restrict__ us = f.u_star + ku;
+            if (i0 > 0) us[0] = o[0];
+            us[1] = o[1];
+            us[2] = o[2];
+            us[3] = o[3];
+            if (i0 + 4 == nx) {
+                const GAcc a{f.u, f.v, ku + 4, kv + 4, W, nx};
+                us[4] = u_pred_val<0, SP>(g, f, dt_override, nx, lj, a);
+            }
+        }
+        if (lj <= v_hi) {
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                o[q] = v_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAccN{ur + r, vr + r, q});
+            float *__restrict__ vs = f.v_star + kv;
+            if (i0 > 0) {
+                *reinterpret_cast<float4 *>(vs) = make_float4(o[0], o[1], o[2], o[3]);
+            } else {
+                vs[1] = o[1];
+                vs[2] = o[2];
+                vs[3] = o[3];
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------ divergence (K3)
 
 // rhs = div(u*, v*) / dt on every owned pressure cell (model.rs:1406-1440).
@@ -1068,6 +1145,23 @@ void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream
     auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
     if (vec && g.scheme == 0 && g.nx % 4 == 0 && a16(f.v) && a16(f.v_star)) {
         const int nbx4 = cdiv(g.nx / 4, kBlock);
+        static const int rpt = [] {
+            // 2 rows per thread: 96 vs 104 (1 row) and 107 us (4 rows), r1 tb_one
+            const char *e = getenv("CFD_PRED_RPT");
+            return e ? atoi(e) : 2;
+        }();
+        if (rpt == 2 || rpt == 4) {
+            const dim3 gr(nbx4 * cdiv(ghi - glo + 1, rpt));
+#define CFD_LAUNCH_PR(SPV, R) hipLaunchKernelGGL((k_predict4r<SPV, R>), gr, dim3(kBlock), 0, s, g, f, \
+                                                 dt_override, glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx4)
+            if (rpt == 2) {
+                if (g.sp_pow2) CFD_LAUNCH_PR(1, 2); else CFD_LAUNCH_PR(0, 2);
+            } else {
+                if (g.sp_pow2) CFD_LAUNCH_PR(1, 4); else CFD_LAUNCH_PR(0, 4);
+            }
+#undef CFD_LAUNCH_PR
+            return;
+        }
         const dim3 grid4(nbx4 * (ghi - glo + 1));
         if (g.sp_pow2)
             hipLaunchKernelGGL(k_predict4<1>, grid4, dim3(kBlock), 0, s, g, f, dt_override,
