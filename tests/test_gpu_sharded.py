@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 
 def run_sharded(n, grid, params, steps, halo_depth):
     import cfdamd
-    os.environ["CFD_HALO_DEPTH"] = str(halo_depth)
+    if halo_depth is not None:   # None: the library's default depth (bench.py's)
+        os.environ["CFD_HALO_DEPTH"] = str(halo_depth)
     hub = cfdamd.LocalHub(n)
     states, models, errors = [None] * n, [None] * n, []
 
@@ -136,3 +137,34 @@ def test_sharded_fused_finish_channel_cylinder(n, tol):
     check_against_oracle(st, grid, dict(scheme=1, inlet_profile=1, jacobi_iters=40,
                                         corrector_passes=0, tol_enabled=int(tol)), 5,
                          FIELDS + ("rhs",))
+
+
+@pytest.mark.parametrize("n,nx,ny,steps", [(2, 8192, 4096, 4), (8, 16384, 8192, 4)])
+def test_sharded_bench_geometry_matches_single_domain(n, nx, ny, steps):
+    """bench.py's exact multi-GPU workloads (C4: 8192x4096 on 2 slabs, C5:
+    16384x8192 on 8 slabs of 16.78 M cells, default halo depth nyl/32 = 32)
+    for 4 timed-mode steps: the assembled slabs equal a single-domain model of
+    the same grid bit for bit (the single domain is itself oracle-exact at the
+    sizes the oracle can run).  Only the transport differs from the N-GPU
+    bench: LocalHub copies instead of RCCL send/recv.  This pins allocation,
+    slab split, row plans and the default depth at full size; four steps from
+    rest leave the rows near the lower slab boundaries at zero, so the halo
+    data itself is checked by the small-grid tests above (non-zero across
+    every boundary, depths 1-8)."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(nx, ny)
+    params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
+    st = run_sharded(n, grid, params, steps, None)
+    assert all(s[3] == 32 for s in st), [s[3] for s in st]
+    got = assemble(st, nx)
+    del st
+    m = cfdamd.Model(grid, params, device=0)
+    try:
+        for _ in range(steps):
+            m.update()
+        ref = m.get_state()
+    finally:
+        m.close()
+    assert np.count_nonzero(ref["p_prime"]) > 0 and np.count_nonzero(ref["u"]) > 0
+    for f in ("u", "v", "p", "p_prime"):
+        assert_bitwise(f"{f} ({n} slabs vs single domain, {nx}x{ny})", got[f], ref[f])
