@@ -80,6 +80,7 @@ struct Geom {
     int32_t tb_kind;      // 1: k_jacobi_tb (T <= 4); prefetch pipeline (T <= 8) with
                           // 3: 4 columns per lane, 4: 2 columns per lane
     int32_t xcd_remap;    // renumber blocks so each XCD gets contiguous tiles (xcd_block)
+    int32_t tb_flip;      // interior segments reverse their march every launch
     // reciprocals of dx, dy, dx*dx, dy*dy; sp_pow2 = 1 when all four spacings
     // are exact powers of two (then sdiv multiplies, bit-identically)
     float r_dx, r_dy, r_dxx, r_dyy;

@@ -786,6 +786,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     }
     g.xcd_remap = 1;
     if (const char *xv = getenv("CFD_XCD_REMAP")) g.xcd_remap = atoi(xv) ? 1 : 0;
+    g.tb_flip = 0;
+    if (const char *fv = getenv("CFD_TB_FLIP")) g.tb_flip = atoi(fv) ? 1 : 0;
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
