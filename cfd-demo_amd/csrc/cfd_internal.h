@@ -97,6 +97,7 @@ struct Fields {
     uint32_t *red_slots;      // spread step maxima (4 x kResSlots)
     uint32_t *vis_slots;      // spread render min/max keys (2 x kResSlots)
     int32_t n_obs;
+    int32_t any_pmask;   // some predictor mask bit (bit 0) is set in this slab's masks
     size_t u_alloc, v_alloc;  // floats in the u/v allocations (incl. ghosts)
     float *u_alloc_base, *v_alloc_base, *u_old_base, *v_old_base, *u_star_base, *v_star_base;
     Ctl *ctl;

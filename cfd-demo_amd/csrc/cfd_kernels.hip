@@ -154,7 +154,7 @@ __device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, floa
     const float laplace = sdiv<SP>(ue1 - 2.0f * uc + uw1, dx * dx, g.r_dxx) +
                           sdiv<SP>(un1 - 2.0f * uc + us1, dy * dy, g.r_dyy);
     float r = uc + dt * (-convective + nu * laplace);
-    if (f.mask_u[(long)lj * W + i] & 1) r = 0.0f;
+    if (f.any_pmask && (f.mask_u[(long)lj * W + i] & 1)) r = 0.0f;
     return r;
 }
 
@@ -229,7 +229,7 @@ __device__ __forceinline__ float v_pred_val(const Geom &g, const Fields &f, floa
         }
     }
     float r;
-    if (f.mask_v[cv] & 1) {
+    if (f.any_pmask && (f.mask_v[cv] & 1)) {
         r = 0.0f;
     } else {
         const float dx = g.dx, dy = g.dy, nu = g.nu;

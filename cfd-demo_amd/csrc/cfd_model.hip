@@ -889,6 +889,12 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.mask_v = m->mask_v;
     f.obs = m->obs;
     f.n_obs = (int32_t)(obs.size() / 2);
+    // without an obstacle in reach the masks are all zero and the predictors
+    // skip their mask loads (a slab can hold mask rows of a cylinder whose
+    // cells lie just outside it, so n_obs alone does not decide this)
+    f.any_pmask = 0;
+    for (uint8_t b : m->h_mask_u) f.any_pmask |= b & 1;
+    for (uint8_t b : m->h_mask_v) f.any_pmask |= b & 1;
     f.ctl = m->ctl;
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
