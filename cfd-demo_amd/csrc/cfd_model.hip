@@ -772,6 +772,18 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // wrap past 2^32 when the row offset is added: slabs up to 1 GiB per field
     if ((uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u > (1ull << 30)) g.tb_kind = 1;
     m->t_max = g.tb_kind == 3 ? 6 : 4;
+    // Once p', p'_new and rhs outgrow the 256 MB Infinity Cache the launch is
+    // HBM-bound and 8 sweeps per launch halve its traffic: 8192^2 on one GPU
+    // runs at 2.33e12 cell-updates/s with T = 8 against 1.38e12 with T = 4
+    // (profiles/r1/single_gpu_large); at 4096^2 (192 MB, cache-resident) T = 4
+    // is faster.  Only with the reciprocal-multiply division: under IEEE
+    // division the march is VALU-bound and T = 8 loses (6144^2: 6.1e11 vs
+    // 7.3e11).  Single-domain models only: sharded slabs keep T = 4.
+    {
+        const uint64_t jac_ws = 3ull * (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u;
+        if (g.tb_kind == 4 && g.fastdiv == 1 && m->n_ranks == 1 && jac_ws > (256ull << 20))
+            m->t_max = 8;
+    }
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
     m->t_max = std::min(m->t_max, g.tb_kind == 1 ? 4 : kMaxTemporal);
     // 24 output rows per wave segment: the best measured geometry at 4096^2

@@ -306,3 +306,14 @@ def test_power_of_two_cavity_uses_reciprocal_multiply():
     m = c.Model(c.cavity_grid(4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
                                                                tol_enabled=False))
     assert m.kernel_config == {"fastdiv": 1, "temporal": 4}
+
+
+def test_beyond_infinity_cache_uses_eight_sweeps_per_launch():
+    """A single-domain grid whose Jacobi working set (p', p'_new, rhs) exceeds
+    the 256 MB Infinity Cache runs 8 sweeps per launch (T = 8 is parity-tested
+    in test_kernel_variants_bitwise); 4096^2 (192 MB) keeps 4."""
+    c = _cfd()
+    m = c.Model(c.cavity_grid(8192, 4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
+                                                                     tol_enabled=False))
+    assert m.kernel_config == {"fastdiv": 1, "temporal": 8}
+    m.close()
