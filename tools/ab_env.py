@@ -15,7 +15,7 @@ for rnd in range(3):
         for kv in filter(None, sp.split(",")):
             k, v = kv.split("=", 1)
             env[k] = v
-        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tb_one.py"), "4096", "5"],
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tb_one.py"), os.environ.get("AB_N", "4096"), "5"],
                              env=env, capture_output=True, text=True, timeout=120)
         if out.returncode != 0:
             print(json.dumps({"setting": sp, "error": out.stderr[-400:]}), flush=True)
