@@ -52,6 +52,10 @@ constexpr int kFarOffset = 0x7FFF0000;   // voffset of a lane that must not touc
 #ifndef CFD_PD4
 #define CFD_PD4 2
 #endif
+// CFD_FORCE_EDGE 1 (diagnostic): every wave takes the boundary-condition path
+#ifndef CFD_FORCE_EDGE
+#define CFD_FORCE_EDGE 0
+#endif
 constexpr int kPipeWaves = CFD_PIPE_WAVES;
 
 // prefetch distance per T: deep enough to cover HBM latency with a short
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(kPipeWaves * 64) void k_jacobi_pipe(
     const int lo_row = w.k_first - 2, hi_row = r1 + T + 2;
     auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
     const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
-    const bool edge = col_edge || row_edge;
+    const bool edge = CFD_FORCE_EDGE || col_edge || row_edge;
     // Interior segments alternate their march direction (odd ones run downward
     // through the mirrored row space — the stencil is symmetric and f32
     // addition commutative, so the bits are the same): neighbouring segments
