@@ -8,10 +8,23 @@ N>1 is the weak-scaling series of SURVEY.md §8(d): every GPU holds a
 N=8: 16384 x 8192), 1D row slabs with RCCL halo exchange over xGMI.
 
 A step = one full Model::update (model.rs:304-379) in the reference's timed
-mode: predictor, divergence, ONE pressure solve of K=200 sweeps (tolerance
-off, no extra corrector passes), corrector, boundaries, residual/CFL
-reductions.  value = global cells x 200 sweeps x steps / max-over-ranks wall
-time of the timed steps (inputs resident in HBM).
+mode: first-order upwind predictor, divergence, ONE pressure solve of K=200
+sweeps (tolerance off, no extra corrector passes), corrector, boundaries,
+residual/CFL reductions.  value = global cells x 200 sweeps x steps /
+max-over-ranks wall time of the timed steps (inputs resident in HBM).
+
+The timed data does not depend on --warmup: every run first develops the
+cavity for --develop (400) untimed steps from rest (97 % of p' non-zero, vs 3 %
+after 20), then runs the W warm-up steps, then times K steps.  After timing, one
+more step runs on the GPU and on the CPU oracle from the same developed state
+and the two are compared bit for bit (`parity_developed_step`).
+
+roofline: `achieved` is the one-pass HBM bytes of a Jacobi launch (read p',
+read rhs, write p' once: 12 B x slab cells) over the measured
+launch time; a launch performs T sweeps on chip, so `algorithmic_sweep_equiv`
+reports the 12 B x cells x T figure separately.  At N=1 a second entry,
+`roofline_control`, times the same kernel family on 8192^2 (T = 8), whose
+768 MB Jacobi working set cannot live in the 256 MB Infinity Cache.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -70,17 +83,7 @@ def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=3):
     threads=1 is the reference's single worker thread (model.rs:1287);
     threads>1 splits the row loops over OpenMP threads, bit-identical results
     (oracle/cfd_oracle.h orc_set_threads)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as orc
-    from oracle import OracleModel
-    orc.set_threads(threads)
-    m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
-                    jacobi_iters=iters, corrector_passes=0, tol_enabled=0)
-    for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
-        m.field(k)[:] = state[k]
-    sc = m.scalars()
-    sc.step, sc.time, sc.dt = state["simulation_step"], state["simulation_time"], state["dt"]
-    m.set_scalars(sc)
+    m, orc = oracle_from_state(nx, ny, iters, re, state, threads)
     m.update()   # untimed warm-up step: touches every page
     steps, t0 = 0, time.perf_counter()
     while True:
@@ -102,6 +105,84 @@ def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=3):
                       + f"; ms/step {1e3 * el / steps:.0f}; host {model}, {ncpu} cpus"}
 
 
+def oracle_from_state(nx, ny, iters, re, state, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    from oracle import OracleModel
+    orc.set_threads(threads)
+    m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
+                    jacobi_iters=iters, corrector_passes=0, tol_enabled=0)
+    for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
+        m.field(k)[:] = state[k]
+    sc = m.scalars()
+    sc.step, sc.time, sc.dt = state["simulation_step"], state["simulation_time"], state["dt"]
+    sc.jacobi_sweeps_total = state["jacobi_sweeps_total"]
+    m.set_scalars(sc)
+    return m, orc
+
+
+def parity_developed_step(model, nx, ny, iters, re, state, threads):
+    """One GPU step and one oracle step from the same developed state; True
+    when every field word and every scalar agree."""
+    import numpy as np
+    o, orc = oracle_from_state(nx, ny, iters, re, state, threads)
+    model.update()
+    o.update()
+    orc.set_threads(1)
+    g = model.get_state()
+    bad = [k for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
+           if not np.array_equal(g[k].view(np.uint32), o.field(k).view(np.uint32))]
+    s = o.scalars()
+    for k, want in (("dt", s.dt), ("last_p_residual", s.p), ("last_u_residual", s.u),
+                    ("last_v_residual", s.v), ("simulation_time", s.time)):
+        if np.float32(g[k]).view(np.uint32) != np.float32(want).view(np.uint32):
+            bad.append(k)
+    return not bad, bad
+
+
+def time_jacobi(model, steps):
+    """Average Jacobi launch time (ms) over `steps` timed-mode steps: HIP events
+    on the model's stream around each step's launch sequence."""
+    model.synchronize()
+    model.timing_begin()
+    model.update_n(steps)
+    tm = model.timing_end()
+    launches = max(steps * model.launches_per_solve(), 1)
+    return tm, tm["solve_ms"] / launches
+
+
+def roofline_entry(model, nx, nyl, launch_ms, bench_kernel_note=None):
+    kern = model.jacobi_kernel
+    T = model.kernel_config["temporal"]
+    cells = nx * nyl
+    one_pass = BYTES_PER_CELL_UPDATE * cells
+    achieved = one_pass / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(kern["name"], f"{nx}x{nyl}")
+    meas = traffic / (launch_ms * 1e-3) / 1e9 if traffic and launch_ms > 0 else None
+    return {
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+        "measured_hbm_GBps": meas,
+        "measured_hbm_frac": meas / HBM_PEAK_GBS if meas else None,
+        "kernel": kern["name"], "slab": [nx, nyl], "sweeps_per_launch": T,
+        "avg_launch_us": launch_ms * 1e3,
+        "us_per_sweep": launch_ms * 1e3 / T,
+        "jacobi_cell_updates_per_s": cells * T / (launch_ms * 1e-3) if launch_ms > 0 else 0.0,
+        "bytes_per_launch": one_pass,
+        "algorithmic_sweep_equiv": {
+            "GBps": achieved * T, "frac": achieved * T / HBM_PEAK_GBS,
+            "note": "12 B per cell-update x T sweeps per launch: the single-sweep figure "
+                    "the launch's on-chip temporal blocking replaces"},
+        "timing": "HIP events on the model stream around each step's Jacobi launch sequence "
+                  "/ launches (includes inter-launch gaps)",
+        "note": "achieved = one-pass bytes (read p', read rhs, write p' once per launch) / "
+                "launch time; traffic = PMC bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, "
+                "gfx950 correction); FETCH_SIZE counts Infinity-Cache hits too "
+                "(MI355X_MICROARCH.md HBM section), so on MALL-resident slabs it is fabric, "
+                "not HBM, traffic",
+    }
+
+
 def pmc_traffic(kernel, slab):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*/pmc_traffic.json, tools/pmc_traffic.py: 2 x FETCH_SIZE +
@@ -119,13 +200,34 @@ def pmc_traffic(kernel, slab):
     return None, None
 
 
+def control_run(args, cfdamd, device, n=8192, steps=10):
+    """The same timed-mode step on an 8192^2 cavity (one GPU): the Jacobi
+    working set (2 p' + rhs = 768 MB) is 3x the Infinity Cache, so its
+    launches stream from HBM; developed for args.develop steps like the main run."""
+    model = cfdamd.Model(cfdamd.cavity_grid(n), cfdamd.SimulationParams.cavity(
+        args.re, args.iters, corrector_passes=0, tol_enabled=False), device=device)
+    model.update_n(args.develop)
+    model.update_n(2)
+    tm, launch_ms = time_jacobi(model, steps)
+    e = roofline_entry(model, n, n, launch_ms)
+    e["workload"] = (f"{n}x{n} cavity Re={args.re:g}, {args.iters} sweeps/step, developed "
+                     f"{args.develop} steps, {steps} timed steps; Jacobi working set "
+                     f"{3 * n * n * 4 / 2**20:.0f} MiB > 256 MiB Infinity Cache")
+    e["ms_per_step"] = tm["step_ms"] / max(tm["steps"], 1)
+    model.close()
+    return e
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     # 400 steps from rest: the fields are developed (97 % of p' non-zero, vs
     # 4 % at step 20), so the timed steps sweep representative data
-    ap.add_argument("--warmup", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=5)
+    # untimed steps from rest before the warm-up, whatever --warmup is: the
+    # timed steps then sweep developed fields (97 % of p' non-zero at 400)
+    ap.add_argument("--develop", type=int, default=400)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--nx", type=int, default=0)
@@ -135,6 +237,9 @@ def main():
                     help="seconds of steps on a scratch model before the measured one is "
                          "created, so the GPU clocks have left their idle state")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-control", action="store_true",
+                    help="skip the 8192^2 (non-MALL-resident) roofline control at N=1")
+    ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,7 +284,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    model.update_n(args.warmup)
+    model.update_n(args.develop + args.warmup)
     barrier()
     model.timing_begin()
     t0 = time.perf_counter()
@@ -195,24 +300,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    res = model.get_residuals()
-    snap = model.get_snapshot()
     import numpy as np
-    finite = bool(np.isfinite(snap.u).all() and np.isfinite(snap.v).all())
+    try:
+        res = model.get_residuals()
+    except cfdamd.CfdError as e:   # CFD_ENONFINITE: reported, not hidden
+        if e.code != cfdamd.CFD_ENONFINITE:
+            raise
+        res = None
     state = model.get_state()   # this rank's slab
+    finite = bool(np.isfinite(state["u"]).all() and np.isfinite(state["v"]).all())
     nonzero = float(np.count_nonzero(state["p_prime"])) / max(state["p_prime"].size, 1)
+    subn = int(((np.abs(state["p_prime"]) > 0) &
+                (np.abs(state["p_prime"]) < np.finfo(np.float32).tiny)).sum())
 
-    cells_local = nx * model.nyl
     kcfg = model.kernel_config
     kern = model.jacobi_kernel
     T = kcfg["temporal"]
     launches = max(args.steps * model.launches_per_solve(), 1)
     launch_ms = tm["solve_ms"] / launches
-    # algorithmic bytes per launch = 12 B/cell-update x cells x sweeps per launch
-    bytes_launch = BYTES_PER_CELL_UPDATE * cells_local * T
-    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-
-    traffic, traffic_src = pmc_traffic(kern["name"], f"{nx}x{model.nyl}")
+    roof = roofline_entry(model, nx, model.nyl, launch_ms)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -227,38 +333,36 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic (lid-driven cavity from rest, build-defined BCs, SURVEY.md §8(d); "
-                    f"timed steps {args.warmup}..{args.warmup + args.steps} on the developed "
-                    f"fields, {100 * nonzero:.0f}% of p' non-zero)",
+                    f"{args.develop} untimed developing steps + {args.warmup} warm-up, timed "
+                    f"steps {args.develop + args.warmup}..{args.develop + args.warmup + args.steps}"
+                    f" on the developed fields: {100 * nonzero:.1f}% of p' non-zero, "
+                    f"{subn} subnormal)",
             "config": {
-                "workload": f"{nx}x{ny} lid-driven cavity Re={args.re:g}, {args.iters} Jacobi "
+                "workload": f"{nx}x{ny} lid-driven cavity Re={args.re:g}, first-order upwind "
+                            f"advection (VelocityScheme::FirstOrder), {args.iters} Jacobi "
                             "sweeps/step, tolerance off, 0 extra corrector passes",
+                "velocity_scheme": "FirstOrder",
                 "grid": [nx, ny], "slab_per_gpu": [nx, model.nyl], "jacobi_iters": args.iters,
                 "parallelism": f"row-slab x{n}" + (f", halo depth {model.halo_depth}" if n > 1 else ""),
                 "kernel": f"{kern['name']} ({T} sweep(s)/launch, kind {kern['kind']})",
                 "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
                              "FMA-corrected (proven exact, 2^32 inputs)"][kcfg["fastdiv"]],
             },
-            "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "traffic_source": traffic_src,
-                # the PMC-measured bytes of this kernel over the same launch time
-                "measured_hbm_GBps": (traffic / (launch_ms * 1e-3) / 1e9
-                                      if traffic and launch_ms > 0 else None),
-                "measured_hbm_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                                      if traffic and launch_ms > 0 else None),
-                "kernel": kern["name"], "sweeps_per_launch": T,
-                "avg_launch_us": launch_ms * 1e3,
-                "algorithmic_bytes_per_launch": bytes_launch,
-                "timing": "HIP events on the model stream around each step's launch sequence, "
-                          "/ launches (includes inter-launch gaps)",
-                "note": "achieved counts 12 B per cell-update (SURVEY §8(d)); with T sweeps "
-                        "per launch the HBM bytes moved are ~1/T of that, so frac > 1 means "
-                        "the kernel beats the single-sweep HBM roofline by on-chip reuse",
-            },
+            "roofline": roof,
             "solve_fraction_of_step": tm["solve_ms"] / tm["step_ms"] if tm["step_ms"] else None,
-            "final_step": res.simulation_step, "final_dt": res.dt, "fields_finite": finite,
+            "final_step": int(state["simulation_step"]), "final_dt": float(state["dt"]),
+            "fields_finite": finite and res is not None,
         }
+        if n == 1 and not args.no_parity and out["fields_finite"]:
+            ok, bad = parity_developed_step(model, nx, ny, args.iters, args.re, state,
+                                            cpu_threads())
+            out["parity_developed_step"] = ok
+            out["parity_developed_step_detail"] = (
+                f"1 step from step {state['simulation_step']} on GPU and oracle "
+                f"(oracle/cfd_oracle.c), every word of u, v, p, u*, v*, p', rhs and the "
+                f"scalars compared" + ("" if ok else f"; differ: {bad}"))
+        if n == 1 and not args.no_control:
+            out["roofline_control"] = control_run(args, cfdamd, local)
         if n == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(nx, ny, args.iters, args.re, args.cpu_budget, state)
             nt = cpu_threads()

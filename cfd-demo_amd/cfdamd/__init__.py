@@ -24,13 +24,14 @@ from typing import List, Optional
 import numpy as np
 
 from . import _lib
-from ._lib import CfdError, CfdGrid, CfdParams, CfdResiduals, CfdState, check, load
+from ._lib import (CFD_ENONFINITE, CfdError, CfdGrid, CfdParams, CfdResiduals, CfdState, check,
+                   load)
 
 __all__ = [
     "VelocityScheme", "InletProfile", "PressureSolver", "BoundaryKind", "Cylinder", "Grid",
     "SimulationParams", "Residuals", "SimSnapshot", "Model", "SimulationControlHandle",
     "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "load", "LocalHub",
-    "VisualizationMode",
+    "VisualizationMode", "CFD_ENONFINITE",
 ]
 
 
@@ -190,6 +191,7 @@ class Model:
         L = load()
         self.grid = grid
         self.params = params
+        self._runner = None   # live SimulationControlHandle: it owns the handle
         self._h = C.c_void_p()
         g, p = grid._c(), params._c()
         if n_ranks == 1:
@@ -223,18 +225,18 @@ class Model:
     # ----------------------------------------------------------------- step
     def update(self) -> None:
         """Model::update (model.rs:304-379); asynchronous."""
-        check("cfd_update", load().cfd_update(self._h))
+        check("cfd_update", load().cfd_update(self._hh()))
 
     def update_n(self, n: int) -> None:
-        check("cfd_update_n", load().cfd_update_n(self._h, n))
+        check("cfd_update_n", load().cfd_update_n(self._hh(), n))
 
     def piso_step(self, dt_sub: float) -> None:
-        check("cfd_piso_step", load().cfd_piso_step(self._h, dt_sub))
+        check("cfd_piso_step", load().cfd_piso_step(self._hh(), dt_sub))
 
     def jacobi_pressure(self) -> float:
         """jacobi_pressure (model.rs:734-824) on the current rhs / p'."""
         r = C.c_float()
-        check("cfd_pressure_solve", load().cfd_pressure_solve(self._h, C.byref(r)))
+        check("cfd_pressure_solve", load().cfd_pressure_solve(self._hh(), C.byref(r)))
         return float(r.value)
 
     def pressure_solve(self) -> float:
@@ -243,16 +245,16 @@ class Model:
         return self.jacobi_pressure()
 
     def run_phase(self, phase: int, dt_sub: float) -> None:
-        check("cfd_run_phase", load().cfd_run_phase(self._h, phase, dt_sub))
+        check("cfd_run_phase", load().cfd_run_phase(self._hh(), phase, dt_sub))
 
     def synchronize(self) -> None:
-        check("cfd_synchronize", load().cfd_synchronize(self._h))
+        check("cfd_synchronize", load().cfd_synchronize(self._hh()))
 
     # --------------------------------------------------------------- params
     def set_parameters(self, params: SimulationParams) -> None:
         """set_parameters (model.rs:1250-1257)."""
         p = params._c()
-        check("cfd_set_params", load().cfd_set_params(self._h, C.byref(p)))
+        check("cfd_set_params", load().cfd_set_params(self._hh(), C.byref(p)))
         self.params = params
 
     # ---------------------------------------------------------------- reads
@@ -262,13 +264,13 @@ class Model:
         u, v, p = (np.empty(n, np.float32) for n in (su, sv, sp))
         dt = C.c_float()
         check("cfd_get_snapshot",
-              load().cfd_get_snapshot(self._h, _fp(u), _fp(v), _fp(p), C.byref(dt)))
+              load().cfd_get_snapshot(self._hh(), _fp(u), _fp(v), _fp(p), C.byref(dt)))
         return SimSnapshot(p=p, u=u, v=v, dt=float(dt.value))
 
     def get_residuals(self) -> Residuals:
         """get_residuals (model.rs:1269-1280)."""
         r = CfdResiduals()
-        check("cfd_get_residuals", load().cfd_get_residuals(self._h, C.byref(r)))
+        check("cfd_get_residuals", load().cfd_get_residuals(self._hh(), C.byref(r)))
         return Residuals(int(r.simulation_step), float(r.simulation_time), float(r.dt),
                          float(r.p), float(r.u), float(r.v), float(r.step_time_s),
                          int(r.piso_substeps), int(r.jacobi_sweeps_total))
@@ -280,7 +282,7 @@ class Model:
                  ("p_prime", sp), ("rhs", sp))}
         st = CfdState(*(_fp(arrs[k]) for k in ("u", "v", "p", "u_star", "v_star", "p_prime",
                                                "rhs")))
-        check("cfd_get_state", load().cfd_get_state(self._h, C.byref(st)))
+        check("cfd_get_state", load().cfd_get_state(self._hh(), C.byref(st)))
         arrs.update(dt=np.float32(st.dt), simulation_time=np.float32(st.simulation_time),
                     simulation_step=int(st.simulation_step),
                     last_p_residual=np.float32(st.last_p_residual),
@@ -307,28 +309,28 @@ class Model:
         st.last_u_residual = float(kw.get("last_u_residual", cur["last_u_residual"]))
         st.last_v_residual = float(kw.get("last_v_residual", cur["last_v_residual"]))
         st.jacobi_sweeps_total = int(kw.get("jacobi_sweeps_total", cur["jacobi_sweeps_total"]))
-        check("cfd_set_state", load().cfd_set_state(self._h, C.byref(st)))
+        check("cfd_set_state", load().cfd_set_state(self._hh(), C.byref(st)))
 
     def get_masks(self):
         su, sv, _ = self._sizes()
         mu, mv = np.empty(su, np.uint8), np.empty(sv, np.uint8)
         check("cfd_get_masks", load().cfd_get_masks(
-            self._h, mu.ctypes.data_as(C.POINTER(C.c_uint8)),
+            self._hh(), mu.ctypes.data_as(C.POINTER(C.c_uint8)),
             mv.ctypes.data_as(C.POINTER(C.c_uint8))))
         return mu, mv
 
     # --------------------------------------------------------------- timing
     def profile_sweeps(self, n: int) -> float:
         ms = C.c_double()
-        check("cfd_profile_sweeps", load().cfd_profile_sweeps(self._h, n, C.byref(ms)))
+        check("cfd_profile_sweeps", load().cfd_profile_sweeps(self._hh(), n, C.byref(ms)))
         return float(ms.value)
 
     def timing_begin(self) -> None:
-        check("cfd_timing_begin", load().cfd_timing_begin(self._h))
+        check("cfd_timing_begin", load().cfd_timing_begin(self._hh()))
 
     def timing_end(self):
         a, b, c, d = C.c_double(), C.c_uint64(), C.c_double(), C.c_uint64()
-        check("cfd_timing_end", load().cfd_timing_end(self._h, C.byref(a), C.byref(b),
+        check("cfd_timing_end", load().cfd_timing_end(self._hh(), C.byref(a), C.byref(b),
                                                       C.byref(c), C.byref(d)))
         return {"solve_ms": a.value, "sweeps": int(b.value), "step_ms": c.value,
                 "steps": int(d.value)}
@@ -337,7 +339,7 @@ class Model:
     def kernel_config(self) -> dict:
         fd, tb = C.c_int(), C.c_int()
         check("cfd_get_kernel_config",
-              load().cfd_get_kernel_config(self._h, C.byref(fd), C.byref(tb)))
+              load().cfd_get_kernel_config(self._hh(), C.byref(fd), C.byref(tb)))
         return {"fastdiv": fd.value, "temporal": tb.value}
 
     # -------------------------------------------------------- visualisation
@@ -347,14 +349,14 @@ class Model:
         img = np.empty((self.nyl, self.grid.nx, 4), np.uint8)
         mm = np.empty(2, np.float32)
         check("cfd_render", load().cfd_render(
-            self._h, int(mode), img.ctypes.data_as(C.POINTER(C.c_uint8)), _fp(mm)))
+            self._hh(), int(mode), img.ctypes.data_as(C.POINTER(C.c_uint8)), _fp(mm)))
         return img, (float(mm[0]), float(mm[1]))
 
     def derive_field(self, mode: "VisualizationMode"):
         """The mode's scalar field (nyl, nx) f32 and its (min, max)."""
         out = np.empty((self.nyl, self.grid.nx), np.float32)
         mm = np.empty(2, np.float32)
-        check("cfd_derive_field", load().cfd_derive_field(self._h, int(mode), _fp(out), _fp(mm)))
+        check("cfd_derive_field", load().cfd_derive_field(self._hh(), int(mode), _fp(out), _fp(mm)))
         return out, (float(mm[0]), float(mm[1]))
 
     def launches_per_solve(self) -> int:
@@ -378,12 +380,12 @@ class Model:
         """Kind and rocprofv3 name of the kernel a fixed-count solve launches."""
         kind, name = C.c_int(), C.create_string_buffer(96)
         check("cfd_get_jacobi_kernel",
-              load().cfd_get_jacobi_kernel(self._h, C.byref(kind), name, 96))
+              load().cfd_get_jacobi_kernel(self._hh(), C.byref(kind), name, 96))
         return {"kind": kind.value, "name": name.value.decode()}
 
     @property
     def halo_depth(self) -> int:
-        return int(load().cfd_get_halo_depth(self._h))
+        return int(load().cfd_get_halo_depth(self._hh()))
 
     # ------------------------------------------------------------------ run
     def run(self) -> "SimulationControlHandle":
@@ -391,7 +393,18 @@ class Model:
         steps it while draining commands."""
         return SimulationControlHandle(self)
 
+    def _hh(self):
+        """The native handle for a direct call: refused while Model.run()'s
+        worker owns it (include/cfd.h: only cfd_run_* until cfd_run_stop)."""
+        if self._runner is not None:
+            raise CfdError("Model", -4, "the model is owned by a running SimulationControlHandle; "
+                                        "stop() it first")
+        return self._h
+
     def close(self) -> None:
+        r = getattr(self, "_runner", None)
+        if r is not None:
+            r.stop()   # the worker must let go of the handle before it is freed
         if getattr(self, "_h", None) and self._h.value:
             load().cfd_destroy(self._h)
             self._h = C.c_void_p()
@@ -411,7 +424,8 @@ class SimulationControlHandle:
     def __init__(self, model: Model):
         self._model = model
         self._r = C.c_void_p()
-        check("cfd_run_start", load().cfd_run_start(model._h, C.byref(self._r)))
+        check("cfd_run_start", load().cfd_run_start(model._hh(), C.byref(self._r)))
+        model._runner = self
 
     def _live(self):
         if not self._r.value:
@@ -423,6 +437,8 @@ class SimulationControlHandle:
         if self._r.value:
             check("cfd_run_stop", load().cfd_run_stop(self._r))
             self._r = C.c_void_p()
+            if self._model._runner is self:
+                self._model._runner = None
 
     def join(self, timeout=None):
         self.stop()

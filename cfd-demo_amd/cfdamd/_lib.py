@@ -76,6 +76,10 @@ class CfdAabb(C.Structure):
     _fields_ = [("center", CfdPoint), ("half_width", C.c_double), ("half_height", C.c_double)]
 
 
+# cfd_status (include/cfd.h)
+CFD_EINVAL, CFD_EHIP, CFD_ERCCL, CFD_ESTATE, CFD_ENONFINITE = -1, -2, -3, -4, -5
+
+
 class CfdError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn} failed ({code}): {msg}")

@@ -34,6 +34,14 @@ __device__ __forceinline__ void publish_max(uint32_t *set, int key, float m) {
     if (m > 0.0f) atomicMax(&set[(key & (kResSlots - 1)) * kResStride], __float_as_uint(m));
 }
 
+// NaN or +-Inf (the step's failure check, SURVEY.md §5: the reference itself
+// has none and keeps stepping on a blown-up field).
+__device__ __forceinline__ bool nonfinite(float x) { return !(fabsf(x) <= 3.40282347e38f); }
+// Raise the step's non-finite flag (Ctl::red[4]); only lanes that saw one store.
+__device__ __forceinline__ void flag_nonfinite(Ctl *c, bool bad) {
+    if (bad) atomicOr(&c->red[4], 1u);
+}
+
 // max(base, every slot of a set); called by all 64 lanes of a wave, uniform result.
 __device__ __forceinline__ float read_max(const uint32_t *set, uint32_t base) {
     const int lane = (int)threadIdx.x & 63;

@@ -49,7 +49,10 @@ struct Ctl {
     uint32_t n_exec_last;   // sweeps executed by the last solve
     float last_p;           // last_pressure_residual
     float res_u, res_v;     // last_u_residual / last_v_residual
-    uint32_t red[4];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|
+    uint32_t red[5];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|; red[4]:
+                            // non-finite flag (1: some new u/v value is NaN or +-Inf)
+    uint32_t nonfinite_step;   // sticky: simulation_step after the first step whose
+                               // velocities were not all finite (0 = never)
     uint32_t vis[2];        // render: max key, max ~key of the derived field (cfd_render.hip)
     uint64_t sweeps_total;
     int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
@@ -101,6 +104,9 @@ struct Fields {
     size_t u_alloc, v_alloc;  // floats in the u/v allocations (incl. ghosts)
     float *u_alloc_base, *v_alloc_base, *u_old_base, *v_old_base, *u_star_base, *v_star_base;
     Ctl *ctl;
+    // host-mapped word (pinned, zero-copy) mirroring Ctl::nonfinite_step, so the
+    // host can see a blown-up run without synchronising the stream
+    uint32_t *host_nonfinite;
 };
 
 // ---- launchers (cfd_kernels.hip) ----

@@ -808,6 +808,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, flo
     Ctl *c = f.ctl;
     const int nx = g.nx, W = nx + 1;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
+    bool bad = false;
     // each block walks a contiguous run of (row, 256-column) tiles, so the
     // residual maxima leave the block as 4 atomics, not 4 per wave per tile
     const long ntiles = (long)nbx * (g.nyl + 1);
@@ -847,6 +848,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, flo
                 f.u[k] = nw;
                 du = fmaxf(du, fabsf(nw - old));
                 mu = fmaxf(mu, fabsf(nw));
+                bad |= nonfinite(nw);
             }
             if (i < nx) {
                 const long k = rp + i;
@@ -863,10 +865,12 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish(Geom g, Fields f, flo
                 f.v[k] = nw;
                 dv = fmaxf(dv, fabsf(nw - old));
                 mv = fmaxf(mv, fabsf(nw));
+                bad |= nonfinite(nw);
                 if (lj < g.nyl) f.p[k] = f.p[k] + pp[k];
             }
         }
     }
+    flag_nonfinite(c, bad);
     __shared__ float red[kBlock / 64][4];
     du = wave_max(du);
     dv = wave_max(dv);
@@ -916,6 +920,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
     Ctl *c = f.ctl;
     const int nx = g.nx, W = nx + 1;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
+    bool bad = false;
     const long ntiles = (long)nbx * (g.nyl + 1);
     const int bid = xcd_block(g), G = (int)gridDim.x;
     const long t_lo = ntiles * bid / G, t_hi = ntiles * (bid + 1) / G;
@@ -954,6 +959,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
             du = fmaxf(fmaxf(fmaxf(du, fabsf(n0 - o0)), fmaxf(fabsf(n1 - o1), fabsf(n2 - o2))),
                        fabsf(n3 - o3));
             mu = fmaxf(fmaxf(fmaxf(mu, fabsf(n0)), fmaxf(fabsf(n1), fabsf(n2))), fabsf(n3));
+            bad |= nonfinite(n0) | nonfinite(n1) | nonfinite(n2) | nonfinite(n3);
             if (i0 + 4 == nx) {   // outflow face nx copies the corrected face nx-1 (Q9)
                 float n4 = cf_u_face<SP>(g, inlet, dt, nx, j, s3, pc.w, pc.z);
                 if (f.n_obs > 0 && (f.mask_u[k + 4] & 2)) n4 = 0.0f;
@@ -961,6 +967,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
                 f.u[k + 4] = n4;
                 du = fmaxf(du, fabsf(n4 - o4));
                 mu = fmaxf(mu, fabsf(n4));
+                bad |= nonfinite(n4);
             }
         }
         float4 nv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -983,6 +990,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
         dv = fmaxf(fmaxf(fmaxf(dv, fabsf(nv.x - ov.x)), fmaxf(fabsf(nv.y - ov.y), fabsf(nv.z - ov.z))),
                    fabsf(nv.w - ov.w));
         mv = fmaxf(fmaxf(fmaxf(mv, fabsf(nv.x)), fmaxf(fabsf(nv.y), fabsf(nv.z))), fabsf(nv.w));
+        bad |= nonfinite(nv.x) | nonfinite(nv.y) | nonfinite(nv.z) | nonfinite(nv.w);
         if (lj < g.nyl) {
             float4 p = *reinterpret_cast<const float4 *>(f.p + rp);
             p.x = p.x + pc.x;
@@ -992,6 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
             *reinterpret_cast<float4 *>(f.p + rp) = p;
         }
     }
+    flag_nonfinite(c, bad);
     __shared__ float red[kBlock / 64][4];
     du = wave_max(du);
     dv = wave_max(dv);
@@ -1023,16 +1032,20 @@ __global__ __launch_bounds__(kBlock) void k_step_reduce(Geom g, Fields f) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     const size_t nu = (size_t)g.nyl * (g.nx + 1), nv = (size_t)(g.nyl + 1) * g.nx;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
+    bool bad = false;
     for (size_t k = tid; k < nu; k += stride) {
         const float a = f.u[k];
         du = fmaxf(du, fabsf(a - f.u_old[k]));
         mu = fmaxf(mu, fabsf(a));
+        bad |= nonfinite(a);
     }
     for (size_t k = tid; k < nv; k += stride) {
         const float a = f.v[k];
         dv = fmaxf(dv, fabsf(a - f.v_old[k]));
         mv = fmaxf(mv, fabsf(a));
+        bad |= nonfinite(a);
     }
+    flag_nonfinite(f.ctl, bad);
     du = wave_max(du);
     dv = wave_max(dv);
     mu = wave_max(mu);
@@ -1061,6 +1074,12 @@ __global__ void k_step_finalize(Geom g, Fields f) {
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
+    // failure detection: red[4] is this step's non-finite flag
+    // (all-reduced across slabs with the maxima); the first such step sticks
+    if (c->red[4] && !c->nonfinite_step) {
+        c->nonfinite_step = c->step + 1u;
+        if (f.host_nonfinite) *f.host_nonfinite = c->step + 1u;   // zero-copy host mirror
+    }
     c->res_u = __uint_as_float(c->red[0]);
     c->res_v = __uint_as_float(c->red[1]);
     const float max_vel = fmaxf(__uint_as_float(c->red[2]), __uint_as_float(c->red[3]));
@@ -1076,7 +1095,7 @@ __global__ void k_step_finalize(Geom g, Fields f) {
         new_dt = fminf(dt_cfl, c->dt);
     }
     c->dt = (new_dt > previous_dt) ? fminf(new_dt, previous_dt * 1.1f) : new_dt;
-    c->red[0] = c->red[1] = c->red[2] = c->red[3] = 0u;
+    c->red[0] = c->red[1] = c->red[2] = c->red[3] = c->red[4] = 0u;
 }
 
 

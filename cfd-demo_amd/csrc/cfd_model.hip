@@ -100,6 +100,7 @@ struct cfd_model {
     Ctl *ctl = nullptr;
     uint32_t *slots = nullptr;   // spread residual maxima (cfd_internal.h kResSlots)
     float *vis_buf = nullptr;    // render output (nx*nyl words), allocated on first use
+    uint32_t *h_nonfinite = nullptr;   // pinned host word the device sets (Fields::host_nonfinite)
     std::vector<uint8_t> h_mask_u, h_mask_v;
     std::vector<uint8_t> dmask_u, dmask_v;   // staging for the async mask upload
     // sharding
@@ -108,6 +109,10 @@ struct cfd_model {
     ncclComm_t comm = nullptr;
     LocalHub *hub = nullptr;   // testing stand-in for comm
     int host_cur = 0;   // mirror of ctl->cur, valid when the tolerance is off
+    // p' ghost rows deeper than 1 are stale (a host-driven tolerance solve or
+    // cfd_profile_sweeps refreshed only one row per sweep): the next deep-halo
+    // fixed-count solve re-exchanges hg rows before its first sweep
+    bool pp_ghosts_shallow = false;
     int t_max = kMaxTemporal;   // sweeps per temporally blocked launch (CFD_TEMPORAL)
     // timing
     hipEvent_t ev_step0 = nullptr, ev_step1 = nullptr, ev_prof0 = nullptr, ev_prof1 = nullptr;
@@ -447,6 +452,11 @@ struct cfd_model {
             // the deep-halo sweeps recompute ghost rows, which read rhs there
             int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
             if (rc0) return rc0;
+            if (pp_ghosts_shallow) {   // sweep 0 reads p' ghosts hg rows deep
+                rc0 = exchange_pp(host_cur, g.hg);
+                if (rc0) return rc0;
+                pp_ghosts_shallow = false;
+            }
             for (int it = 0; it < iters;) {
                 int T, lo, hi, exch;
                 plan_block(g.j0, g.nyl, g.ny, g.hg, it, tmax, iters, &T, &lo, &hi, &exch);
@@ -506,6 +516,7 @@ struct cfd_model {
         launch_finalize_solve(g, f, -1, iters, 0, n, stream);
         HIP_TRY(hipGetLastError());
         host_cur = (host_cur + n) & 1;
+        pp_ghosts_shallow = true;
         float res = 0.f;
         HIP_TRY(hipMemcpyAsync(&res, &f.ctl->last_p, 4, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
@@ -576,7 +587,7 @@ struct cfd_model {
         if (rc) return rc;
         if (!fused) launch_step_reduce(g, f, stream);
         if (sharded()) launch_fold_slots(f.ctl->red, f.red_slots, 4, stream);
-        rc = allreduce_max_u32(f.ctl->red, 4);
+        rc = allreduce_max_u32(f.ctl->red, 5);   // maxima + the non-finite flag
         if (rc) return rc;
         launch_step_finalize(g, f, stream);
         HIP_TRY(hipGetLastError());
@@ -615,6 +626,7 @@ struct cfd_model {
                           (void *)obs, (void *)ctl, (void *)slots, (void *)vis_buf,
                           (void *)mg_pool, (void *)mg_dev})
             if (ptr) (void)hipFree(ptr);
+        if (h_nonfinite) (void)hipHostFree(h_nonfinite);
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (ev_step0) (void)hipEventDestroy(ev_step0);
         if (ev_step1) (void)hipEventDestroy(ev_step1);
@@ -829,6 +841,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         (rc = zalloc((void **)&m->ctl, sizeof(Ctl))) ||
         (rc = zalloc((void **)&m->slots, kSlotWords * 4)))
         return rc;
+    HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 4, hipHostMallocMapped | hipHostMallocCoherent));
+    *(volatile uint32_t *)m->h_nonfinite = 0u;
 
     // obstacle masks and cell list from cell centres (model.rs:235-260)
     std::vector<uint8_t> mu(nyl * W, 0), mv((nyl + 1) * nx, 0);
@@ -908,6 +922,11 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     for (uint8_t b : m->h_mask_u) f.any_pmask |= b & 1;
     for (uint8_t b : m->h_mask_v) f.any_pmask |= b & 1;
     f.ctl = m->ctl;
+    {
+        void *dp = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dp, m->h_nonfinite, 0));
+        f.host_nonfinite = (uint32_t *)dp;
+    }
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
     f.vis_slots = f.red_slots + (size_t)4 * kResSlots * kResStride;
@@ -988,6 +1007,16 @@ const char *cfd_last_error(void) { return g_last_error.c_str(); }
 // internal (not in cfd.h): lets the host runtime (cfd_runtime.cpp) report
 // through the same thread-local message
 void cfdrt_set_error(const char *msg) { g_last_error = msg ? msg : ""; }
+// internal: the host-only checks cfd_set_params makes, for cfd_run_set_params
+// to reject bad parameters synchronously (reads only the immutable grid)
+int cfdrt_check_params(const cfd_model *m, const cfd_params *p) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    int rc = validate(&m->grid, p);
+    if (rc) return rc;
+    if (m->sharded() && p->pressure_solver != CFD_SOLVER_JACOBI)
+        return fail(CFD_EINVAL, "SOR and multigrid solvers run on unsharded models only");
+    return 0;
+}
 
 int cfd_get_config(const cfd_model *m, cfd_grid *grid, cfd_params *params) {
     if (!m) return fail(CFD_EINVAL, "null model");
@@ -1072,6 +1101,11 @@ int cfd_update(cfd_model *m) { return cfd_update_n(m, 1); }
 int cfd_update_n(cfd_model *m, int n) {
     if (!m) return fail(CFD_EINVAL, "null model");
     HIP_TRY(hipSetDevice(m->device));
+    // failure detection: a step the device has already finished left a NaN or
+    // Inf in u/v (zero-copy word, no stream synchronisation)
+    if (const uint32_t bad = *(volatile uint32_t *)m->h_nonfinite)
+        return fail(CFD_ENONFINITE, "non-finite velocity (NaN/Inf) after step " + std::to_string(bad) +
+                                        "; cfd_set_state clears it");
     for (int k = 0; k < n; ++k) {
         int rc = m->enqueue_update();
         if (rc) return rc;
@@ -1241,6 +1275,9 @@ int cfd_get_residuals(cfd_model *m, cfd_residuals *out) {
         out->step_time_s = ms * 1e-3;
     else
         out->step_time_s = 0.0;
+    if (c.nonfinite_step)   // *out is filled all the same
+        return fail(CFD_ENONFINITE, "non-finite velocity (NaN/Inf) after step " +
+                                        std::to_string(c.nonfinite_step));
     return 0;
 }
 
@@ -1287,7 +1324,10 @@ int cfd_set_state(cfd_model *m, const cfd_state *st) {
     c.res_u = st->last_u_residual;
     c.res_v = st->last_v_residual;
     c.sweeps_total = st->jacobi_sweeps_total;
+    c.nonfinite_step = 0;   // a new state: failure detection starts over
+    c.red[4] = 0;
     HIP_TRY(hipMemcpy(m->f.ctl, &c, offsetof(Ctl, go), hipMemcpyHostToDevice));
+    *(volatile uint32_t *)m->h_nonfinite = 0u;
     m->host_cur = c.cur;
     // ghosts of the injected slab
     rc = m->exchange_uv();
@@ -1324,6 +1364,7 @@ int cfd_profile_sweeps(cfd_model *m, int n_sweeps, double *avg_ms_out) {
     launch_finalize_solve(g, m->f, -1, n_sweeps, 0, n_sweeps, m->stream);
     HIP_TRY(hipGetLastError());
     m->host_cur = (m->host_cur + n_sweeps) & 1;
+    m->pp_ghosts_shallow = m->sharded();   // owned rows only were swept
     int rc = m->sync();
     if (rc) return rc;
     float ms = 0.f;

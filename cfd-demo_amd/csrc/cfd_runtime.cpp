@@ -29,6 +29,7 @@
 #include "../../include/cfd.h"
 
 extern "C" void cfdrt_set_error(const char *msg);   // cfd_model.hip (internal)
+extern "C" int cfdrt_check_params(const cfd_model *m, const cfd_params *p);   // ditto
 
 namespace {
 
@@ -209,7 +210,10 @@ int cfd_run_resume(cfd_runner *r) {
 }
 
 int cfd_run_set_params(cfd_runner *r, const cfd_params *p) {
-    if (!p) return run_fail(CFD_EINVAL, "null params");
+    if (!r || !p) return run_fail(CFD_EINVAL, "null runner or params");
+    // the reference's set_parameters cannot fail (model.rs:1250-1257): reject
+    // what cfd_set_params would reject here, before the worker sees it
+    if (int rc = cfdrt_check_params(r->model, p)) return rc;
     Cmd c{};
     c.kind = CMD_PARAMS;
     c.params = *p;

@@ -45,6 +45,10 @@ typedef enum {
     CFD_EHIP = -2,     /* HIP runtime error (no device, out of memory, launch) */
     CFD_ERCCL = -3,    /* RCCL error (sharded models only) */
     CFD_ESTATE = -4,   /* call not valid in the model's current state */
+    CFD_ENONFINITE = -5, /* a finished step left NaN/Inf in u or v (failure detection;
+                            the reference has none): cfd_update refuses to step on
+                            and cfd_get_residuals reports it (filling *out all the
+                            same) until cfd_set_state injects a new state */
 } cfd_status;
 
 typedef struct cfd_model cfd_model;

@@ -168,3 +168,55 @@ def test_sharded_bench_geometry_matches_single_domain(n, nx, ny, steps):
     assert np.count_nonzero(ref["p_prime"]) > 0 and np.count_nonzero(ref["u"]) > 0
     for f in ("u", "v", "p", "p_prime"):
         assert_bitwise(f"{f} ({n} slabs vs single domain, {nx}x{ny})", got[f], ref[f])
+
+
+def test_sharded_tolerance_toggle_keeps_deep_ghosts():
+    """set_parameters flips the tolerance on (host-driven solves refresh one
+    p' ghost row per sweep) and back off (deep-halo fixed-count solves read
+    hg ghost rows): the fixed-count solve after the toggle must re-exchange
+    the deep ghosts first, or the slabs drift from the single domain."""
+    import cfdamd
+    from oracle import OracleModel
+    n, depth = 3, 6
+    grid = cfdamd.cavity_grid(96, 96)
+    fixed = cfdamd.SimulationParams.cavity(100.0, 24, corrector_passes=1, tol_enabled=False)
+    tol = cfdamd.SimulationParams.cavity(100.0, 24, corrector_passes=1, tol_enabled=True)
+    schedule = [fixed, fixed, tol, tol, fixed, fixed, fixed]
+    os.environ["CFD_HALO_DEPTH"] = str(depth)
+    hub = cfdamd.LocalHub(n)
+    states, models, errors = [None] * n, [None] * n, []
+
+    def worker(r):
+        try:
+            m = cfdamd.Model(grid, schedule[0], device=0, n_ranks=n, rank=r, local_hub=hub)
+            models[r] = m
+            for k, p in enumerate(schedule):
+                if k and p is not schedule[k - 1]:
+                    m.set_parameters(p)
+                m.update()
+            m.synchronize()
+            states[r] = (m.j0, m.j1, m.get_state(), m.halo_depth)
+        except Exception as e:
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    for m in models:
+        if m is not None:
+            m.close()
+    hub.close()
+    os.environ.pop("CFD_HALO_DEPTH", None)
+    if errors:
+        raise errors[0]
+    kw = dict(bc_kind=1, viscosity=0.01, jacobi_iters=24, corrector_passes=1)
+    o = OracleModel(96, 96, 1.0, 1.0, tol_enabled=0, **kw)
+    for k, p in enumerate(schedule):
+        if k and p is not schedule[k - 1]:
+            o.set_params(tol_enabled=int(p.tol_enabled), **kw)
+        o.update()
+    got = assemble(states, 96)
+    for f in FIELDS:
+        assert_bitwise(f"toggle:{f}", got[f], o.field(f))
