@@ -68,18 +68,27 @@ def test_runtime_steps_pauses_snapshots_and_stops():
     assert_bitwise("snapshot p", s.p, o2.field("p"))
 
 
-def test_runtime_reports_worker_failure():
-    """A worker call that fails (invalid parameters) is reported, not hidden;
-    the worker stops stepping and still stops cleanly."""
+def test_runtime_rejects_bad_params_synchronously():
+    """The reference's set_parameters cannot fail (model.rs:1250-1257), so
+    parameters the model would refuse are rejected by cfd_run_set_params
+    itself, before the worker sees them: the caller gets the error, the
+    model's parameters are unchanged and the worker keeps stepping.  (A
+    worker that fails mid-run, e.g. on a non-finite field, is reported by
+    cfd_run_status: tests/test_gpu_long.py::test_nonfinite_velocity_is_reported.)"""
     import cfdamd
     m = cfdamd.Model(cfdamd.Grid(32, 16, 1.0, 1.0), cfdamd.SimulationParams())
     h = m.run()
+    before = m.params
     bad = cfdamd.SimulationParams(jacobi_iters=10 ** 6)
-    h.set_params(bad)
-    _wait(lambda: h.status()[0] != 0)
-    rc, msg = h.status()
-    assert rc == -1 and "jacobi_iters" in msg
+    with pytest.raises(cfdamd.CfdError) as e:
+        h.set_params(bad)
+    assert e.value.code == -1 and "jacobi_iters" in str(e.value)
+    assert m.params is before
     n = h.steps
-    time.sleep(0.05)
-    assert h.steps == n
+    _wait(lambda: h.steps > n + 2)
+    assert h.status()[0] == 0
+    with pytest.raises(cfdamd.CfdError):   # the worker owns the handle
+        m.update()
     h.stop()
+    m.update()                               # handed back after stop
+    m.close()
