@@ -81,7 +81,8 @@ struct Geom {
     int32_t tb_bpc;       // target k_jacobi_tb blocks per CU (balanced segmentation)
     int32_t n_cu;         // compute units of the device
     int32_t tb_kind;      // 1: k_jacobi_tb (T <= 4); prefetch pipeline (T <= 8) with
-                          // 3: 4 columns per lane, 4: 2 columns per lane
+                          // 3: 4 columns per lane, 4: 2 columns per lane; 5: the
+                          // 2-column march with its rhs window in LDS
     int32_t xcd_remap;    // renumber blocks so each XCD gets contiguous tiles (xcd_block)
     int32_t tb_flip;      // interior segments reverse their march every launch
     // reciprocals of dx, dy, dx*dx, dy*dy; sp_pow2 = 1 when all four spacings
@@ -141,6 +142,9 @@ void launch_pipe4(const Geom &g, const Fields &f, int T, int pass, int it, int p
                   int out_hi, uint32_t *res_slots, hipStream_t s);
 void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
                   int out_hi, uint32_t *res_slots, hipStream_t s);
+// kind 5: the same march with its rhs window in LDS (cfd_jacobi_lds.hip, T <= 8)
+void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
+                int out_hi, uint32_t *res_slots, hipStream_t s);
 // dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before
 // an all-reduce of dst reads it).
 void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s);

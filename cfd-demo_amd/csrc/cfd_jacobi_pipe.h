@@ -52,6 +52,13 @@ constexpr int kFarOffset = 0x7FFF0000;   // voffset of a lane that must not touc
 #ifndef CFD_PD4
 #define CFD_PD4 2
 #endif
+#ifndef CFD_PD8
+#define CFD_PD8 4
+#endif
+// CFD_PIPE_WPE > 0: minimum waves per SIMD the register allocation must allow
+#ifndef CFD_PIPE_WPE
+#define CFD_PIPE_WPE 0
+#endif
 // CFD_FORCE_EDGE 1 (diagnostic): every wave takes the boundary-condition path
 #ifndef CFD_FORCE_EDGE
 #define CFD_FORCE_EDGE 0
@@ -60,7 +67,8 @@ constexpr int kPipeWaves = CFD_PIPE_WAVES;
 
 // prefetch distance per T: deep enough to cover HBM latency with a short
 // unroll period U = lcm(3, PD, T+PD)
-template <int T> struct PipeDepth { static constexpr int PD = 4; };   // T 2: U 12; T 8: U 12
+template <int T> struct PipeDepth { static constexpr int PD = 4; };   // T 2: U 12
+template <> struct PipeDepth<8> { static constexpr int PD = CFD_PD8; };  // PD 4: U 12
 template <> struct PipeDepth<1> { static constexpr int PD = 2; };     // U 6
 template <> struct PipeDepth<3> { static constexpr int PD = 3; };     // U 6
 template <> struct PipeDepth<4> { static constexpr int PD = CFD_PD4; };  // PD 2: U 6
@@ -264,8 +272,13 @@ struct Pipe {
     }
 };
 
+#if CFD_PIPE_WPE > 0
+#define CFD_PIPE_BOUNDS __launch_bounds__(kPipeWaves * 64, CFD_PIPE_WPE)
+#else
+#define CFD_PIPE_BOUNDS __launch_bounds__(kPipeWaves * 64)
+#endif
 template <int T, int FAST, int VEC>
-__global__ __launch_bounds__(kPipeWaves * 64) void k_jacobi_pipe(
+__global__ CFD_PIPE_BOUNDS void k_jacobi_pipe(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int it, int par, int out_lo, int out_hi, int nwc,
     int nseg) {

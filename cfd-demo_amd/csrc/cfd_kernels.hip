@@ -1241,6 +1241,8 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
         launch_pipe4(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else if (g.tb_kind == 4)
         launch_pipe2(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
+    else if (g.tb_kind == 5)
+        launch_lds(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else
         launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
 }

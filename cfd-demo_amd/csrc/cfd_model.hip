@@ -778,7 +778,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     g.tb_kind = 4;
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
-        g.tb_kind = (k == 3 || k == 4) ? k : 1;
+        g.tb_kind = (k == 3 || k == 4 || k == 5) ? k : 1;
     }
     // the pipelined kernels park masked lanes at a far voffset that must not
     // wrap past 2^32 when the row offset is added: slabs up to 1 GiB per field
@@ -795,6 +795,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         const uint64_t jac_ws = 3ull * (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u;
         if (g.tb_kind == 4 && g.fastdiv == 1 && m->n_ranks == 1 && jac_ws > (256ull << 20))
             m->t_max = 8;
+        if (g.tb_kind == 5) m->t_max = 8;
     }
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
     m->t_max = std::min(m->t_max, g.tb_kind == 1 ? 4 : kMaxTemporal);
@@ -1435,6 +1436,8 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
             snprintf(buf, sizeof buf, "k_jacobi<%d, %d>", kJacRowsPerWave, m->g.fastdiv);
         else if (k == 1)
             snprintf(buf, sizeof buf, "k_jacobi_tb<%d, %d>", T, m->g.fastdiv);
+        else if (k == 5)
+            snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, false>", T, m->g.fastdiv);
         else
             snprintf(buf, sizeof buf, "k_jacobi_pipe<%d, %d, %d>", T, m->g.fastdiv, k == 3 ? 4 : 2);
         snprintf(name, name_len, "%s", buf);

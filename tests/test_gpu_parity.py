@@ -267,10 +267,13 @@ def test_control_handle_run_loop():
     ("1", "4", "3"), ("1", "3", "3"), ("1", "2", "3"), ("1", "1", "3"), ("2", "8", "3"),
     ("2", "4", "1"), ("1", "6", "4"), ("1", "8", "4"), ("0", "8", "4"), ("1", "4", "4"),
     ("1", "7", "4"), ("1", "5", "4"), ("1", "3", "4"), ("1", "2", "4"), ("1", "1", "4"),
-    ("2", "6", "4")])
+    ("2", "6", "4"),
+    ("1", "8", "5"), ("1", "7", "5"), ("1", "6", "5"), ("1", "5", "5"), ("1", "4", "5"),
+    ("1", "3", "5"), ("1", "2", "5"), ("1", "1", "5"), ("0", "8", "5"), ("2", "8", "5"),
+    ("0", "4", "5"), ("2", "5", "5")])
 def test_kernel_variants_bitwise(monkeypatch, fastdiv, temporal, kind):
     """Every Jacobi kernel variant (IEEE or proven-exact fast division; 1..8
-    sweeps per launch; kinds 1, 3 and 4) gives the oracle's bits, on a power-of-two cavity (where
+    sweeps per launch; kinds 1, 3, 4 and 5) gives the oracle's bits, on a power-of-two cavity (where
     the reciprocal multiply is exact) and on the reference's default channel
     grid (non-power-of-two divisors)."""
     c = _cfd()
