@@ -31,19 +31,27 @@ namespace {
 
 constexpr int kLdsWaves = 4;   // waves per workgroup (256 threads)
 #ifndef CFD_LDS_SB
-#define CFD_LDS_SB 1   // scheduling barrier between slots (bounds live ranges)
+#define CFD_LDS_SB 0   // scheduling barriers: 1 between slots, 2 also between stages
+#endif                 // (bound live ranges; measured no faster, r2 ab_lds_R*.log)
+#ifndef CFD_LDS_PD
+#define CFD_LDS_PD 3   // prefetch distance (slots) of the p' and rhs rows
 #endif
 #ifndef CFD_LDS_WPE
 #define CFD_LDS_WPE 0  // > 0: minimum waves per SIMD for the register allocation
 #endif
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int ring_depth(int T) { return ((T + 1 + 2) / 3) * 3; }   // multiple of 3, >= T+1
+constexpr int lds_gcd(int a, int b) { return b == 0 ? a : lds_gcd(b, a % b); }
+// rhs ring depth: the smallest multiple of lcm(3, PD) that holds T+1 rows
+constexpr int ring_depth(int T, int PD) {
+    const int q = 3 / lds_gcd(3, PD) * PD;
+    return ((T + 1 + q - 1) / q) * q;
+}
 
 template <int T, int FAST, bool RES>
 struct LdsMarch {
-    static constexpr int PD = 3;                // prefetch distance (slots) of p' and rhs
-    static constexpr int D = ring_depth(T);     // rhs ring depth (rows); PD and 3 divide it
+    static constexpr int PD = CFD_LDS_PD;       // prefetch distance (slots) of p' and rhs
+    static constexpr int D = ring_depth(T, PD); // rhs ring depth (rows); PD and 3 divide it
     static constexpr int U = D;                 // slot unroll: every ring index compile-time
     static constexpr int H = (T + 1) / 2;       // halo lanes per side (2 columns per lane)
     static constexpr int OUTL = 64 - 2 * H;     // lanes whose columns are stored
@@ -57,7 +65,7 @@ struct LdsMarch {
     int k_first, S, lo_clamp, hi_clamp, nch, g_first, g_last, g_top, g_zero, row_bytes;
     int ch, vo_ld, vo_st, abase, dir;
     bool e0, e1;         // residual columns (EDGE waves)
-    float dx_sq, dy_sq, denom, r_dx_sq, r_dy_sq, r_denom;
+    const Geom *g;       // the kernel argument: divisors and their reciprocals
     __amdgpu_buffer_rsrc_t rs_p, rs_r, rs_d;
     float m;
 
@@ -87,9 +95,9 @@ struct LdsMarch {
         const float hy = C.x + from_right(C.x);
         const f2 h = {hx, hy};
         const f2 v = Tp + B;
-        const f2 hz = fdiv2<FAST>(h, dx_sq, r_dx_sq);
-        const f2 vt = fdiv2<FAST>(v, dy_sq, r_dy_sq);
-        const f2 pu = fdiv2<FAST>(hz + vt - Rh, denom, r_denom);
+        const f2 hz = fdiv2<FAST>(h, g->dx_sq, g->r_dx_sq);
+        const f2 vt = fdiv2<FAST>(v, g->dy_sq, g->r_dy_sq);
+        const f2 pu = fdiv2<FAST>(hz + vt - Rh, g->denom, g->r_denom);
         const float omega = 0.75f;
         const float om1 = 1.0f - omega;
         return omega * pu + om1 * C;
@@ -110,7 +118,7 @@ struct LdsMarch {
     template <int V_, int GUARD, bool EDGE>
     __device__ __forceinline__ void slot(int v) {
         if (GUARD == 2 && v >= S) return;
-        if (CFD_LDS_SB) __builtin_amdgcn_sched_barrier(0);
+        if (CFD_LDS_SB >= 1) __builtin_amdgcn_sched_barrier(0);
         const int k = k_first + v;
         W[0][V_ % 3] = PQ[V_ % PD];                                  // input row k
         PQ[V_ % PD] = ld(rs_p, k + PD);
@@ -119,6 +127,7 @@ struct LdsMarch {
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
             if (GUARD == 0 && V_ < 2 * s) continue;                  // compile-time
+            if (CFD_LDS_SB >= 2 && s > 1) __builtin_amdgcn_sched_barrier(0);
             const int r = k - s;
             const float2 rh = ring[((V_ - s + 8 * D) % D) * 64 + lane];
             const f2 &B = W[s - 1][(V_ + 1) % 3];                    // stage s-1, row r-1
@@ -221,12 +230,7 @@ __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
     w.rs_d = __builtin_amdgcn_make_buffer_rsrc(dst_alloc, 0, pbytes, 0x00020000);
     w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)g.hg * nx), 0, pbytes,
                                                0x00020000);
-    w.dx_sq = g.dx_sq;
-    w.dy_sq = g.dy_sq;
-    w.denom = g.denom;
-    w.r_dx_sq = g.r_dx_sq;
-    w.r_dy_sq = g.r_dy_sq;
-    w.r_denom = g.r_denom;
+    w.g = &g;
     // residual columns 1..=nx-8 (the reference's full 8-lane chunks, Q6)
     w.e0 = out_lane && col >= 1 && col <= nx - 8;
     w.e1 = out_lane && col + 1 >= 1 && col + 1 <= nx - 8;

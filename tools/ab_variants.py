@@ -9,7 +9,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 names = sys.argv[1:]
 best = {}
-for rnd in range(3):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
     for nm in names:
         lib = os.path.join(ROOT, "cfd-demo_amd", "lib", "variants", nm, "libcfd_amd.so")
         env = dict(os.environ, CFD_LIB=lib)

@@ -13,7 +13,7 @@ for c in "${LIST[@]}"; do
   name="k${K}_t${T}_r${R}"
   echo "=== $name $(date +%T)"
   CFD_TB_KIND=$K CFD_TEMPORAL=$T CFD_TB_ROWS=$R timeout -s KILL 150 \
-    rocprofv3 --pmc $CTRS --kernel-include-regex "k_jacobi_pipe" -d gpurun_out/pmc_$TAG \
+    rocprofv3 --pmc $CTRS --kernel-include-regex "k_jacobi_(pipe|lds)" -d gpurun_out/pmc_$TAG \
     -o ${name} --output-format csv -- python3 tools/tb_one.py 4096 1 \
     > gpurun_out/pmc_$TAG/${name}.log 2>&1
   rc=$?
