@@ -19,7 +19,7 @@ EXPORTS = [
     "cfd_pressure_solve", "cfd_run_phase", "cfd_set_params", "cfd_get_snapshot",
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
-    "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block",
+    "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block", "cfd_plan_overlap",
     "cfd_render", "cfd_derive_field", "cfd_last_error", "cfd_abi_version", "cfd_destroy",
     "cfd_get_config", "cfd_run_start", "cfd_run_stop", "cfd_run_pause", "cfd_run_resume",
     "cfd_run_set_params", "cfd_run_request_snapshot", "cfd_run_last_snapshot",
@@ -136,6 +136,7 @@ def load():
         "cfd_plan_sweep": (i32, [i32, i32, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i32),
                                  C.POINTER(i32)]),
         "cfd_plan_halo": (i32, [i32, i32, i32, i32, i32, C.POINTER(i32)]),
+        "cfd_plan_overlap": (i32, [i32, i32, i32, i32, i32, i32, C.POINTER(i32)]),
         "cfd_plan_block": (i32, [i32, i32, i32, i32, i32, i32, i32, C.POINTER(i32),
                                  C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "cfd_render": (i32, [vp, i32, C.POINTER(C.c_uint8), FP]),
@@ -187,6 +188,8 @@ def load():
         "cfd_mesh_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("CFD_LIB") and not hasattr(L, name):
+            continue   # an older tuning variant (tools/build_variants.sh) may predate a symbol
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -11,9 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -87,6 +89,11 @@ enum FieldId { FLD_U = 0, FLD_V, FLD_PP0, FLD_PP1, FLD_RHS };
 struct cfd_model {
     int device = 0;
     hipStream_t stream = nullptr;
+    // sharded fixed-count solves: the boundary bands and their p' exchange run
+    // on cstream while the interior runs on stream (SURVEY.md §8(e) overlap)
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_ov0 = nullptr, ev_ov1 = nullptr;
+    bool overlap = true;   // CFD_OVERLAP=0 serialises them
     cfd_grid grid{};
     cfd_params params{};
     Geom g{};
@@ -101,6 +108,12 @@ struct cfd_model {
     uint32_t *slots = nullptr;   // spread residual maxima (cfd_internal.h kResSlots)
     float *vis_buf = nullptr;    // render output (nx*nyl words), allocated on first use
     uint32_t *h_nonfinite = nullptr;   // pinned host word the device sets (Fields::host_nonfinite)
+    // sharded tolerance mode: per-sweep residuals copied to pinned host words,
+    // each with its completion event (kLag ring, see enqueue_solve_host_driven)
+    static constexpr int kResRing = 8;
+    uint32_t *h_res = nullptr;
+    hipEvent_t ev_res[kResRing] = {};
+    double rccl_timeout_s = 300.0;      // CFD_RCCL_TIMEOUT_S
     std::vector<uint8_t> h_mask_u, h_mask_v;
     std::vector<uint8_t> dmask_u, dmask_v;   // staging for the async mask upload
     // sharding
@@ -156,9 +169,11 @@ struct cfd_model {
 
     // Ghost-row exchange of one field with both neighbours (geometry from
     // plan_halo): one RCCL group of at most two sends and two receives.
-    int exchange(int id, int kind, int depth) {
+    int exchange(int id, int kind, int depth, hipStream_t st = nullptr) {
         if (!sharded()) return 0;
-        if (hub) return exchange_local(id, kind, depth);
+        if (!st) st = stream;
+        if (hub) return exchange_local(id, kind, depth, st);
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
         float *base = field_ptr(id);
         const size_t pitch = field_pitch(id);
         int h[6];
@@ -166,23 +181,23 @@ struct cfd_model {
         RCCL_TRY(ncclGroupStart());
         if (h[2] > 0) {
             RCCL_TRY(ncclSend(base + (long)h[0] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
-                              rank - 1, comm, stream));
+                              rank - 1, comm, st));
             RCCL_TRY(ncclRecv(base + (long)h[1] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
-                              rank - 1, comm, stream));
+                              rank - 1, comm, st));
         }
         if (h[5] > 0) {
             RCCL_TRY(ncclSend(base + (long)h[3] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
-                              rank + 1, comm, stream));
+                              rank + 1, comm, st));
             RCCL_TRY(ncclRecv(base + (long)h[4] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
-                              rank + 1, comm, stream));
+                              rank + 1, comm, st));
         }
         RCCL_TRY(ncclGroupEnd());
         return 0;
     }
 
     // LocalHub form: copy the neighbours' send rows straight into our ghosts.
-    int exchange_local(int id, int kind, int depth) {
-        HIP_TRY(hipStreamSynchronize(stream));
+    int exchange_local(int id, int kind, int depth, hipStream_t st) {
+        HIP_TRY(hipStreamSynchronize(st));
         hub->barrier();   // every member's rows are final
         float *base = field_ptr(id);
         const size_t pitch = field_pitch(id);
@@ -197,9 +212,9 @@ struct cfd_model {
             const int psend = side == 0 ? ph[3] : ph[0];   // peer's rows facing us
             HIP_TRY(hipMemcpyAsync(base + (long)h[3 * side + 1] * (long)pitch,
                                    peer->field_ptr(id) + (long)psend * (long)pitch,
-                                   (size_t)rows * pitch * 4, hipMemcpyDeviceToDevice, stream));
+                                   (size_t)rows * pitch * 4, hipMemcpyDeviceToDevice, st));
         }
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipStreamSynchronize(st));
         hub->barrier();   // nobody overwrites rows a peer is still copying
         return 0;
     }
@@ -212,7 +227,9 @@ struct cfd_model {
     }
 
     // p' halo: `rows` owned boundary rows of buffer `buf` each way.
-    int exchange_pp(int buf, int rows) { return exchange(buf ? FLD_PP1 : FLD_PP0, HALO_PP, rows); }
+    int exchange_pp(int buf, int rows, hipStream_t st = nullptr) {
+        return exchange(buf ? FLD_PP1 : FLD_PP0, HALO_PP, rows, st);
+    }
 
     int allreduce_max_u32(uint32_t *dev, size_t n) {
         if (!sharded()) return 0;
@@ -230,9 +247,48 @@ struct cfd_model {
             HIP_TRY(hipMemcpy(dev, acc.data(), n * 4, hipMemcpyHostToDevice));
             return 0;
         }
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
         RCCL_TRY(ncclAllReduce(dev, dev, n, ncclUint32, ncclMax, comm, stream));
         return 0;
     }
+
+    // Wait for the stream (ev == nullptr) or for one event, with the RCCL
+    // communicator watched: a peer that failed (ncclCommGetAsyncError) or made
+    // no progress for CFD_RCCL_TIMEOUT_S seconds aborts the communicator and
+    // fails with CFD_ERCCL instead of blocking forever.
+    int wait_done(hipEvent_t ev) {
+        if (!comm) {
+            HIP_TRY(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(stream));
+            return 0;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0;; ++spin) {
+            const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(stream);
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady)
+                return fail(CFD_EHIP, std::string("stream/event query: ") + hipGetErrorString(q));
+            ncclResult_t ar = ncclSuccess;
+            const ncclResult_t r = ncclCommGetAsyncError(comm, &ar);
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (r != ncclSuccess || ar != ncclSuccess || el > rccl_timeout_s) {
+                const std::string why = (r != ncclSuccess || ar != ncclSuccess)
+                                            ? std::string("RCCL asynchronous error: ") +
+                                                  ncclGetErrorString(r != ncclSuccess ? r : ar)
+                                            : "RCCL exchange made no progress for " +
+                                                  std::to_string((int)rccl_timeout_s) + " s";
+                ncclCommAbort(comm);
+                comm = nullptr;
+                comm_aborted = true;
+                return fail(CFD_ERCCL, why + " (rank " + std::to_string(rank) +
+                                           "); the communicator was aborted");
+            }
+            if (spin < 256)
+                std::this_thread::yield();
+            else
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    bool comm_aborted = false;
 
     // -------------------------------------------------------------- solve
     // jacobi_pressure (model.rs:734-824).  Unsharded: one launch per sweep
@@ -461,13 +517,32 @@ struct cfd_model {
                 int T, lo, hi, exch;
                 plan_block(g.j0, g.nyl, g.ny, g.hg, it, tmax, iters, &T, &lo, &hi, &exch);
                 const int res = it + T == iters;
-                if (tmax == 1)
+                // Overlap: the block before an exchange first
+                // computes the hg-row bands the exchange sends, on cstream, which
+                // then runs the exchange, while the interior rows run on stream.
+                // Ghost rows need no compute here: the exchange replaces them.
+                int ov[6];
+                const bool ovl = overlap && exch && tmax > 1 &&
+                                 plan_overlap(g.nyl, g.hg, rank, n_ranks, lo, hi, ov);
+                if (ovl) {
+                    HIP_TRY(hipEventRecord(ev_ov0, stream));
+                    HIP_TRY(hipStreamWaitEvent(cstream, ev_ov0, 0));
+                    for (int b = 0; b < 2; ++b)   // empty bands launch nothing
+                        launch_jacobi_block(g, f, pass, it, launches, T, ov[2 * b], ov[2 * b + 1], res,
+                                            cstream);
+                    launch_jacobi_block(g, f, pass, it, launches, T, ov[4], ov[5], res, stream);
+                    int rc = exchange_pp((host_cur + launches + 1) & 1, g.hg, cstream);
+                    if (rc) return rc;
+                    HIP_TRY(hipEventRecord(ev_ov1, cstream));
+                    HIP_TRY(hipStreamWaitEvent(stream, ev_ov1, 0));
+                } else if (tmax == 1) {
                     launch_jacobi_sweep(g, f, pass, it, lo, hi, res, stream);
-                else
+                } else {
                     launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, res, stream);
+                }
                 it += T;
                 ++launches;
-                if (exch) {
+                if (exch && !ovl) {
                     int rc = exchange_pp((host_cur + launches) & 1, g.hg);
                     if (rc) return rc;
                 }
@@ -490,13 +565,33 @@ struct cfd_model {
         return 0;
     }
 
-    // Sharded with the tolerance on: the host follows the reference's control
-    // flow, reading the all-reduced residual after every sweep (halo depth 1).
+    // Sharded with the tolerance on: the reference's early exit (model.rs:816)
+    // needs the all-reduced residual of every sweep.  Sweep k's residual is
+    // copied to a pinned host word behind its all-reduce; the host enqueues
+    // sweep k+1 (kernel, residual fold, all-reduce, 1-row p' exchange) BEFORE
+    // it waits for sweep k's word, so the GPU and the xGMI link never idle on
+    // the host's decision (one-sweep-lagged convergence).  When sweep k has
+    // converged, sweep k+1 is already queued: its kernel reads sweep k's
+    // all-reduced residual on the device and returns without writing
+    // (k_jacobi's early exit), so p' and the sweep count are the reference's;
+    // only its all-reduce and exchange of an untouched buffer run in vain.
     int enqueue_solve_host_driven(float *residual_out) {
         const int iters = params.jacobi_iters;
         const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
-        int n = 0;
-        for (int it = 0; it < iters; ++it) {
+        constexpr int kLag = 1;
+        static_assert(kLag < kResRing, "lag ring");
+        int n = iters;   // sweeps the reference executes
+        auto converged = [&](int k, bool *yes) -> int {
+            int rc = wait_done(ev_res[k % kResRing]);
+            if (rc) return rc;
+            float e;
+            std::memcpy(&e, (const void *)&h_res[k % kResRing], 4);
+            *yes = e < params.p_tol;
+            return 0;
+        };
+        int checked = 0;   // sweeps whose residual the host has read
+        bool done = false;
+        for (int it = 0; it < iters && !done; ++it) {
             launch_jacobi_sweep(g, f, -1, it, lo, hi, 1, stream);
             launch_fold_slots(f.ctl->err + it, f.err_slots + (size_t)it * kResSlots * kResStride, 1,
                               stream);
@@ -504,14 +599,31 @@ struct cfd_model {
             if (rc) return rc;
             rc = exchange_pp((host_cur + it + 1) & 1, 1);
             if (rc) return rc;
-            ++n;
-            uint32_t bits = 0;
-            HIP_TRY(hipMemcpyAsync(&bits, f.ctl->err + it, 4, hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));
-            float e;
-            std::memcpy(&e, &bits, 4);
-            if (params.tol_enabled && e < params.p_tol) break;
+            HIP_TRY(hipMemcpyAsync(&h_res[it % kResRing], f.ctl->err + it, 4, hipMemcpyDeviceToHost,
+                                   stream));
+            HIP_TRY(hipEventRecord(ev_res[it % kResRing], stream));
+            while (checked <= it - kLag && !done) {
+                bool yes = false;
+                rc = converged(checked, &yes);
+                if (rc) return rc;
+                if (yes) {
+                    n = checked + 1;
+                    done = true;
+                }
+                ++checked;
+            }
         }
+        while (!done && checked < iters) {
+            bool yes = false;
+            int rc = converged(checked, &yes);
+            if (rc) return rc;
+            if (yes) {
+                n = checked + 1;
+                done = true;
+            }
+            ++checked;
+        }
+        if (iters == 0) n = 0;
         // the device finalize recomputes n from the (identical) all-reduced slots
         launch_finalize_solve(g, f, -1, iters, 0, n, stream);
         HIP_TRY(hipGetLastError());
@@ -519,7 +631,8 @@ struct cfd_model {
         pp_ghosts_shallow = true;
         float res = 0.f;
         HIP_TRY(hipMemcpyAsync(&res, &f.ctl->last_p, 4, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
+        int rc = wait_done(nullptr);
+        if (rc) return rc;
         if (residual_out) *residual_out = res;
         return 0;
     }
@@ -605,8 +718,7 @@ struct cfd_model {
 
     int sync() {
         HIP_TRY(hipSetDevice(device));
-        HIP_TRY(hipStreamSynchronize(stream));
-        return 0;
+        return wait_done(nullptr);
     }
 
     int read_ctl(Ctl *out) {
@@ -620,6 +732,9 @@ struct cfd_model {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm) ncclCommDestroy(comm);
+        for (hipEvent_t e : ev_res)
+            if (e) (void)hipEventDestroy(e);
+        if (h_res) (void)hipHostFree(h_res);
         for (void *ptr : {(void *)u_all, (void *)v_all, (void *)uo_all, (void *)vo_all,
                           (void *)us_all, (void *)vs_all, (void *)p, (void *)rhs,
                           (void *)pp_all[0], (void *)pp_all[1], (void *)mask_u, (void *)mask_v,
@@ -633,6 +748,9 @@ struct cfd_model {
         if (ev_prof0) (void)hipEventDestroy(ev_prof0);
         if (ev_prof1) (void)hipEventDestroy(ev_prof1);
         if (stream) (void)hipStreamDestroy(stream);
+        if (cstream) (void)hipStreamDestroy(cstream);
+        if (ev_ov0) (void)hipEventDestroy(ev_ov0);
+        if (ev_ov1) (void)hipEventDestroy(ev_ov1);
     }
 };
 
@@ -728,6 +846,10 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     m->grid = *grid;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&m->cstream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&m->ev_ov0, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&m->ev_ov1, hipEventDisableTiming));
+    if (const char *ov = getenv("CFD_OVERLAP")) m->overlap = atoi(ov) != 0;
     HIP_TRY(hipEventCreate(&m->ev_step0));
     HIP_TRY(hipEventCreate(&m->ev_step1));
     HIP_TRY(hipEventCreate(&m->ev_prof0));
@@ -775,7 +897,14 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // kind 4 (prefetch-pipelined march, 2 columns per lane) at T = 4 is the
     // fastest measured geometry on the bench workload (tools/tune_tb.py, r1:
     // 8.45 us/sweep vs 11.05 for kind 1 and 11.3 for kind 3 at its best T)
-    g.tb_kind = 4;
+    // Default Jacobi march (measured at 4096^2 on developed fields, r2:
+    // profiles/r2/tune_r2b_kind5.log, ab_lds_*.log): with the proven-exact
+    // reciprocal multiply, kind 5 (rhs window in LDS, DPP-folded sums) at
+    // T = 8 sweeps per launch and 40-row segments, 6.42 us per sweep, against
+    // 7.75 for kind 4 at T = 8 and 9.04 at T = 4; under IEEE (or FMA-corrected)
+    // division the march is VALU-bound and kind 4 at T = 4 stays (r1: 6144^2
+    // 7.3e11 vs 6.1e11 cell-updates/s at T = 8).  Single domain and slabs alike.
+    g.tb_kind = g.fastdiv == 1 ? 5 : 4;
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
         g.tb_kind = (k == 3 || k == 4 || k == 5) ? k : 1;
@@ -784,14 +913,9 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // wrap past 2^32 when the row offset is added: slabs up to 1 GiB per field
     if ((uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u > (1ull << 30)) g.tb_kind = 1;
     m->t_max = g.tb_kind == 3 ? 6 : 4;
-    // Once p', p'_new and rhs outgrow the 256 MB Infinity Cache the launch is
-    // HBM-bound and 8 sweeps per launch halve its traffic: 8192^2 on one GPU
-    // runs at 2.33e12 cell-updates/s with T = 8 against 1.38e12 with T = 4
-    // (profiles/r1/single_gpu_large); at 4096^2 (192 MB, cache-resident) T = 4
-    // is faster.  Only with the reciprocal-multiply division: under IEEE
-    // division the march is VALU-bound and T = 8 loses (6144^2: 6.1e11 vs
-    // 7.3e11).  Single-domain models only: sharded slabs keep T = 4.
     {
+        // kind 4 past the 256 MB Infinity Cache: 8 sweeps per launch halve the
+        // HBM traffic (8192^2: 2.33e12 vs 1.38e12 cell-updates/s, r1)
         const uint64_t jac_ws = 3ull * (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u;
         if (g.tb_kind == 4 && g.fastdiv == 1 && m->n_ranks == 1 && jac_ws > (256ull << 20))
             m->t_max = 8;
@@ -799,10 +923,9 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     }
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
     m->t_max = std::min(m->t_max, g.tb_kind == 1 ? 4 : kMaxTemporal);
-    // 24 output rows per wave segment: the best measured geometry at 4096^2
-    // (tools/tune_tb.py; segments whose slot count is a multiple of the
-    // 12-slot unrolled march avoid the remainder group)
-    g.tb_rows = 24;
+    // output rows per wave segment: 24 for kind 4 (12-slot unrolled march),
+    // 40 for kind 5 (4096^2: 6.42 us/sweep vs 6.50 at 32 and 6.68 at 24)
+    g.tb_rows = g.tb_kind == 5 ? 40 : 24;
     if (const char *rv = getenv("CFD_TB_ROWS")) g.tb_rows = std::max(4, std::min(1024, atoi(rv)));
     g.tb_bpc = 3;
     if (const char *bv = getenv("CFD_TB_BPC")) {   // balanced segmentation instead
@@ -844,6 +967,9 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         return rc;
     HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 4, hipHostMallocMapped | hipHostMallocCoherent));
     *(volatile uint32_t *)m->h_nonfinite = 0u;
+    HIP_TRY(hipHostMalloc((void **)&m->h_res, 4 * cfd_model::kResRing, hipHostMallocDefault));
+    for (hipEvent_t &e : m->ev_res) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (const char *to = getenv("CFD_RCCL_TIMEOUT_S")) m->rccl_timeout_s = std::max(1.0, atof(to));
 
     // obstacle masks and cell list from cell centres (model.rs:235-260)
     std::vector<uint8_t> mu(nyl * W, 0), mv((nyl + 1) * nx, 0);
@@ -1240,7 +1366,7 @@ int render_common(cfd_model *m, int mode, bool field, void *host_out, float *min
     HIP_TRY(hipMemcpyAsync(keys, f.ctl->vis, 8, hipMemcpyDeviceToHost, m->stream));
     HIP_TRY(hipMemsetAsync(f.ctl->vis, 0, 8, m->stream));
     if (host_out) HIP_TRY(hipMemcpyAsync(host_out, m->vis_buf, n * 4, hipMemcpyDeviceToHost, m->stream));
-    HIP_TRY(hipStreamSynchronize(m->stream));
+    if (int rc2 = m->wait_done(nullptr)) return rc2;
     if (min_max_out) {
         min_max_out[0] = decode_key(keys[1], true);
         min_max_out[1] = decode_key(keys[0], false);
@@ -1466,6 +1592,11 @@ int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, i
         return fail(CFD_EINVAL, "bad plan_block arguments");
     plan_block(j0, nyl, ny, halo_depth, it, t_max, iters, T, out_lo, out_hi, exchange);
     return 0;
+}
+
+int cfd_plan_overlap(int nyl, int halo_depth, int rank, int n_ranks, int lo, int hi, int *out6) {
+    if (!out6 || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad plan_overlap arguments");
+    return plan_overlap(nyl, halo_depth, rank, n_ranks, lo, hi, out6);
 }
 
 int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6) {

@@ -57,6 +57,25 @@ inline void plan_block(int j0, int nyl, int ny, int hg, int it, int t_max, int i
     *exchange = ex;
 }
 
+// Overlapped exchange block (SURVEY.md §8(e) overlap plan): the block that
+// ends with a p' exchange is split into the bands the exchange sends — rows
+// [0, hg) to rank-1 and [nyl-hg, nyl) to rank+1, computed first, then
+// exchanged while the rest runs — and the interior rows.  Ghost rows of the
+// block's range [lo, hi) are not computed: the exchange replaces them.
+// out6 = {band_lo[0], band_hi[0], band_lo[1], band_hi[1], in_lo, in_hi}, an
+// empty band (lo == hi) where there is no neighbour; returns 0 when the slab
+// is too thin to split (then the block runs whole, exchange after it).
+inline int plan_overlap(int nyl, int hg, int rank, int n_ranks, int lo, int hi, int out6[6]) {
+    const bool below = rank > 0, above = rank < n_ranks - 1;
+    out6[0] = 0;
+    out6[1] = below ? hg : 0;
+    out6[2] = above ? nyl - hg : nyl;
+    out6[3] = nyl;
+    out6[4] = below ? hg : lo;
+    out6[5] = above ? nyl - hg : hi;
+    return out6[5] > out6[4] ? 1 : 0;
+}
+
 // Halo geometry for one field, in local rows:
 //   out[0..2] = {send_start, recv_start, rows} with the rank below (rank-1)
 //   out[3..5] = {send_start, recv_start, rows} with the rank above (rank+1)

@@ -214,6 +214,11 @@ int cfd_plan_slab(uint64_t ny, int n_ranks, int rank, uint64_t *j0, uint64_t *j1
 int cfd_plan_sweep(int j0, int nyl, int ny, int halo_depth, int it, int iters, int *lo, int *hi,
                    int *exchange);
 int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6);
+/* The overlapped exchange block: out6 = the two bands the
+ * p' exchange sends ({lo, hi} to rank-1, then to rank+1; empty without a
+ * neighbour) and the interior {lo, hi} computed while it travels; returns 1
+ * when the block splits, 0 when the slab is too thin (run it whole). */
+int cfd_plan_overlap(int nyl, int halo_depth, int rank, int n_ranks, int lo, int hi, int *out6);
 /* Temporally blocked form of cfd_plan_sweep: the launch starting at sweep
  * `it` runs *T <= t_max sweeps and stores its last sweep on local rows
  * [out_lo, out_hi); halo_depth <= 0 means unsharded. */

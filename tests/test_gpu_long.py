@@ -81,7 +81,7 @@ def test_c2_timed_mode_bitwise():
     no extra corrector passes (the bench's timed mode at C2); scalars every
     step, the whole state at steps 4 and 10."""
     m, o = cavity(1024, 1024, 400.0, jacobi_iters=100, corrector_passes=0, tol_enabled=False)
-    assert m.kernel_config == {"fastdiv": 1, "temporal": 4}
+    assert m.kernel_config == {"fastdiv": 1, "temporal": 8}
     for step in range(1, 11):
         m.update()
         o.update()
@@ -156,16 +156,22 @@ def test_long_horizon_bitwise_through_subnormals(name):
 
 # ------------------------------------------------------ developed states
 
-@pytest.mark.parametrize("n,develop,temporal,nz_min", [(4096, 400, 4, 0.9), (8192, 400, 8, 0.25)])
-def test_step_from_developed_state_bitwise(n, develop, temporal, nz_min):
-    """The bench workloads (4096^2: T = 4 sweeps per launch, MALL-resident;
-    8192^2: T = 8) developed on the GPU, then ONE more step on the GPU and on
-    the oracle from the same state; every field bitwise."""
+@pytest.mark.parametrize("n,develop,kind,temporal,nz_min", [
+    (4096, 400, None, 8, 0.9), (4096, 400, "4", 4, 0.9), (8192, 400, None, 8, 0.25)])
+def test_step_from_developed_state_bitwise(monkeypatch, n, develop, kind, temporal, nz_min):
+    """The bench workloads developed on the GPU (4096^2 with the default march,
+    kind 5 at T = 8, MALL-resident, and with kind 4 at T = 4; 8192^2, whose
+    Jacobi working set is 3x the Infinity Cache), then ONE more step on the
+    GPU and on the oracle from the same state; every field bitwise."""
     import cfdamd
     from oracle import OracleModel
+    if kind:
+        monkeypatch.setenv("CFD_TB_KIND", kind)
+        monkeypatch.setenv("CFD_TEMPORAL", str(temporal))
     m = cfdamd.Model(cfdamd.cavity_grid(n), cfdamd.SimulationParams.cavity(
         1000.0, 200, corrector_passes=0, tol_enabled=False))
     assert m.kernel_config["temporal"] == temporal
+    assert m.jacobi_kernel["kind"] == (int(kind) if kind else 5)
     m.update_n(develop)
     st = m.get_state()
     nz = np.count_nonzero(st["p_prime"]) / st["p_prime"].size

@@ -305,18 +305,32 @@ def test_kernel_variants_bitwise(monkeypatch, fastdiv, temporal, kind):
 
 
 def test_power_of_two_cavity_uses_reciprocal_multiply():
+    """The bench grid proves the reciprocal multiply exact and so runs the
+    default march: kind 5 (rhs window in LDS) at 8 sweeps per launch."""
     c = _cfd()
     m = c.Model(c.cavity_grid(4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
                                                                tol_enabled=False))
-    assert m.kernel_config == {"fastdiv": 1, "temporal": 4}
-
-
-def test_beyond_infinity_cache_uses_eight_sweeps_per_launch():
-    """A single-domain grid whose Jacobi working set (p', p'_new, rhs) exceeds
-    the 256 MB Infinity Cache runs 8 sweeps per launch (T = 8 is parity-tested
-    in test_kernel_variants_bitwise); 4096^2 (192 MB) keeps 4."""
-    c = _cfd()
-    m = c.Model(c.cavity_grid(8192, 4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
-                                                                     tol_enabled=False))
     assert m.kernel_config == {"fastdiv": 1, "temporal": 8}
+    assert m.jacobi_kernel == {"kind": 5, "name": "k_jacobi_lds<8, 1, false>"}
+
+
+def test_kernel_selection_rules(monkeypatch):
+    """Kind 4 keeps T = 4 inside the 256 MB Infinity Cache and goes to T = 8
+    beyond it (its launch is then HBM-bound); IEEE division (a grid whose
+    divisors have no proven-exact reciprocal form, CFD_FASTDIV=0 here) keeps
+    kind 4 at T = 4.  Every variant is parity-tested in
+    test_kernel_variants_bitwise."""
+    c = _cfd()
+    p = c.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
+    monkeypatch.setenv("CFD_TB_KIND", "4")
+    m = c.Model(c.cavity_grid(8192, 4096), p)
+    assert m.kernel_config == {"fastdiv": 1, "temporal": 8}
+    m.close()
+    m = c.Model(c.cavity_grid(4096), p)
+    assert m.kernel_config == {"fastdiv": 1, "temporal": 4}
+    m.close()
+    monkeypatch.delenv("CFD_TB_KIND")
+    monkeypatch.setenv("CFD_FASTDIV", "0")
+    m = c.Model(c.cavity_grid(1024), p)
+    assert m.kernel_config == {"fastdiv": 0, "temporal": 4} and m.jacobi_kernel["kind"] == 4
     m.close()

@@ -53,6 +53,25 @@ def plan_block(j0, nyl, ny, hg, it, t_max, iters):
     return T.value, lo.value, hi.value, bool(ex.value)
 
 
+def plan_overlap(nyl, hg, r, n, lo, hi):
+    out = (C.c_int * 6)()
+    split = _lib().cfd_plan_overlap(nyl, hg, r, n, lo, hi, out)
+    return bool(split), list(out)
+
+
+def block_band(src, rhs, g0, a, b, T, nx, ny, j0, dx, dy):
+    """The final sweep of a T-sweep block, stored rows [a, b) only, from src
+    alone: what one launch of the temporally blocked kernel over [a, b)
+    computes (its intermediate sweeps live on chip, here in private copies)."""
+    cur, nxt = src.copy(), src.copy()
+    for s_ in range(T):
+        e = T - 1 - s_
+        lo_, hi_ = max(a - e, 1 - j0), min(b + e, ny - 1 - j0)
+        sweep_rows(cur, nxt, rhs, g0, lo_, hi_, nx, ny, j0, dx, dy)
+        cur, nxt = nxt, cur
+    return cur
+
+
 def plan_halo(kind, nyl, depth, r, n):
     out = (C.c_int * 6)()
     assert _lib().cfd_plan_halo(kind, nyl, depth, r, n, out) == 0
@@ -100,13 +119,39 @@ def exchange(arr, g0, spec, rank, n):
         q.wait()
 
 
+def exchange_start(arr, g0, spec, rank, n):
+    """Post the sends of the band rows and the receives of the ghost rows
+    (non-blocking, like the RCCL group on the comm stream)."""
+    sends, recvs = [], []
+    for peer, (s, rcv, rows) in ((rank - 1, spec[0:3]), (rank + 1, spec[3:6])):
+        if rows == 0:
+            continue
+        buf = torch.from_numpy(np.ascontiguousarray(arr[s + g0:s + g0 + rows]))
+        sends.append(dist.isend(buf, peer))
+    for peer, (s, rcv, rows) in ((rank - 1, spec[0:3]), (rank + 1, spec[3:6])):
+        if rows == 0:
+            continue
+        buf = torch.empty((rows, arr.shape[1]), dtype=torch.float32)
+        recvs.append((dist.irecv(buf, peer), buf, rcv))
+    return sends, recvs
+
+
+def exchange_finish(arr, g0, pend):
+    sends, recvs = pend
+    for q, buf, rcv in recvs:
+        q.wait()
+        arr[rcv + g0:rcv + g0 + buf.shape[0]] = buf.numpy()
+    for q in sends:
+        q.wait()
+
+
 def _worker(rank, n, port, cases, results):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=n)
     try:
         out = []
-        for (nx, ny, hg, iters, seed, t_max) in cases:
+        for (nx, ny, hg, iters, seed, t_max, ovl) in cases:
             rng = np.random.default_rng(seed)
             P = rng.uniform(-1, 1, (ny, nx)).astype(F)
             RHS = rng.uniform(-1, 1, (ny, nx)).astype(F)
@@ -134,6 +179,33 @@ def _worker(rank, n, port, cases, results):
                     # k_jacobi_tb: T sweeps, sweep s recomputing T-1-s extra rows
                     # each side of the stored band (clipped to global 1..ny-2)
                     T, lo, hi, ex = plan_block(j0, nyl, ny, hg, it, t_max, iters)
+                    split, ov = plan_overlap(nyl, hg, rank, n, lo, hi) if (ovl and ex) else (False, None)
+                    if split:
+                        # the overlapped schedule of cfd_model.hip: bands the
+                        # exchange sends first, their exchange in flight while
+                        # the interior is computed, then the wait
+                        src, dst = bufs[cur], bufs[cur ^ 1]
+                        for b in range(2):
+                            a_, b_ = ov[2 * b], ov[2 * b + 1]
+                            if b_ > a_:
+                                band = block_band(src, rhs, g0, a_, b_, T, nx, ny, j0, dx, dy)
+                                dst[a_ + g0:b_ + g0] = band[a_ + g0:b_ + g0]
+                                if j0 + a_ <= 1 < j0 + b_:       # fused P(i,0) = P(i,1) store
+                                    dst[g0 - j0] = band[g0 - j0]
+                                if j0 + a_ <= ny - 2 < j0 + b_:  # fused P(i,ny-1) store
+                                    dst[g0 + ny - 1 - j0] = band[g0 + ny - 1 - j0]
+                        pend = exchange_start(dst, g0, plan_halo(2, nyl, hg, rank, n), rank, n)
+                        a_, b_ = ov[4], ov[5]
+                        inner = block_band(src, rhs, g0, a_, b_, T, nx, ny, j0, dx, dy)
+                        dst[a_ + g0:b_ + g0] = inner[a_ + g0:b_ + g0]
+                        if j0 + a_ <= 1 < j0 + b_:
+                            dst[g0 - j0] = inner[g0 - j0]
+                        if j0 + a_ <= ny - 2 < j0 + b_:
+                            dst[g0 + ny - 1 - j0] = inner[g0 + ny - 1 - j0]
+                        exchange_finish(dst, g0, pend)
+                        cur ^= 1
+                        it += T
+                        continue
                     for s_ in range(T):
                         e = T - 1 - s_
                         a, b = max(lo - e, 1 - j0), min(hi + e, ny - 1 - j0)
@@ -179,16 +251,20 @@ def _free_port():
     return p
 
 
-CASES = [  # nx, ny, halo depth, sweeps, seed, sweeps per launch
-    (16, 40, 1, 5, 1, 1),
-    (24, 40, 3, 7, 2, 1),
-    (32, 44, 8, 20, 3, 1),
-    (16, 30, 4, 4, 4, 1),
-    (16, 37, 2, 9, 5, 1),
-    (16, 40, 8, 21, 6, 4),
-    (24, 44, 6, 13, 7, 4),
-    (16, 37, 3, 10, 8, 2),
-    (16, 40, 5, 12, 9, 3),
+CASES = [  # nx, ny, halo depth, sweeps, seed, sweeps per launch, overlapped exchange
+    (16, 40, 1, 5, 1, 1, 0),
+    (24, 40, 3, 7, 2, 1, 0),
+    (32, 44, 8, 20, 3, 1, 0),
+    (16, 30, 4, 4, 4, 1, 0),
+    (16, 37, 2, 9, 5, 1, 0),
+    (16, 40, 8, 21, 6, 4, 0),
+    (24, 44, 6, 13, 7, 4, 0),
+    (16, 37, 3, 10, 8, 2, 0),
+    (16, 40, 5, 12, 9, 3, 0),
+    (16, 40, 4, 21, 10, 4, 1),
+    (24, 44, 6, 13, 11, 4, 1),
+    (16, 37, 3, 10, 12, 2, 1),
+    (16, 48, 8, 25, 13, 8, 1),
 ]
 
 
@@ -207,7 +283,7 @@ def test_sharded_jacobi_plan_matches_single_domain(n):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for (nx, ny, hg, iters, seed, _), res in zip(CASES, got):
+    for (nx, ny, hg, iters, seed, _, _), res in zip(CASES, got):
         rng = np.random.default_rng(seed)
         P = rng.uniform(-1, 1, (ny, nx)).astype(F)
         RHS = rng.uniform(-1, 1, (ny, nx)).astype(F)
