@@ -26,9 +26,14 @@ if [ "${TUNE:-0}" = 1 ]; then
 fi
 if [ "${PROFILE:-1}" = 1 ]; then
   export TMPDIR=/tmp
-  step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --no-cpu-baseline --no-parity
+  # the bench's main workload alone (its 8192^2 control launches the same
+  # kernel name, so it gets its own trace: the stats then average one size each)
+  step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control
+  step rocprof_control 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o control --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control --nx 8192 --ny 8192 --steps 10
 fi
 if [ "${PMC:-0}" = 1 ]; then
+  # dispatch budget: 30 developing steps = ~1,000 dispatches (< 1 ms of
+  # counter collection each, r2), one counter group per run
   export TMPDIR=/tmp
   step pmc_fetch 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_$TAG -o fetch --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2
   step pmc_write 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_$TAG -o write --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2

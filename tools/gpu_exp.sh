@@ -1,20 +1,24 @@
-# Full GPU parity suite on the new defaults, then PMC traffic of the default
-# march at 4096^2 and 8192^2 (dispatch-budgeted: 30 developing steps), then
-# the bench under a kernel trace.
+# (1) the RCCL transport through the socket network on one GPU (two ranks,
+# own NCCL_HOSTID each); (2) the r1 "PMC hang" command shape, timed: a full
+# developed bench run (~12k dispatches) under one WRITE_SIZE pass.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-step() { local name=$1 secs=$2; shift 2; echo "=== $name $(date +%T)"; local t0=$(date +%s.%N)
-  timeout -k 10 "$secs" "$@" > gpurun_out/$name.log 2>&1; local rc=$?
-  echo "=== $name rc=$rc $(python3 -c "print(round($(date +%s.%N)-$t0,1))") s"; tail -3 gpurun_out/$name.log
-  [ $rc -eq 0 ] || exit $rc; }
-step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
-for N in 4096 8192; do
-  A="--no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2 --nx $N --ny $N"
-  step pmc_fetch_$N 170 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_r2c_$N -o fetch --output-format csv -- python3 bench.py $A
-  step pmc_write_$N 170 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_r2c_$N -o write --output-format csv -- python3 bench.py $A
-  python3 tools/pmc_traffic.py gpurun_out/pmc_r2c_$N/fetch_counter_collection.csv gpurun_out/pmc_r2c_$N/write_counter_collection.csv --workload ${N}x${N} --command "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate runs) -- python3 bench.py $A" -o gpurun_out/pmc_r2c_$N/pmc_traffic.json
-done
-step bench 600 python bench.py
-step rocprof_stats 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r2c -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-parity
-echo DONE
+echo "=== rccl_loopback $(date +%T)"
+NCCL_DEBUG=WARN timeout -k 10 280 python3 tools/rccl_loopback.py --n 2 --steps 4 > gpurun_out/rccl_loopback.log 2>&1
+rc=$?; echo "rc=$rc"; tail -20 gpurun_out/rccl_loopback.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+echo "=== pmc_long $(date +%T)"
+t0=$(date +%s)
+timeout -s KILL 160 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_long -o write --output-format csv -- python3 bench.py --no-cpu-baseline --no-parity --no-control > gpurun_out/pmc_long.log 2>&1
+rc=$?; echo "rc=$rc wall=$(( $(date +%s) - t0 )) s"; tail -2 gpurun_out/pmc_long.log | cut -c1-300
+python3 - <<'PY'
+import csv, collections
+try:
+    rows = list(csv.DictReader(open("gpurun_out/pmc_long/write_counter_collection.csv")))
+    d = collections.Counter(r["Dispatch_Id"] for r in rows)
+    ts = sorted(int(r["Start_Timestamp"]) for r in rows)
+    print("dispatches", len(d), "span_s", (ts[-1] - ts[0]) / 1e9 if ts else None)
+except Exception as e:
+    print("no csv", e)
+PY
