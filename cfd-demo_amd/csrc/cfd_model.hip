@@ -923,9 +923,11 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     }
     if (const char *tv = getenv("CFD_TEMPORAL")) m->t_max = std::max(1, atoi(tv));
     m->t_max = std::min(m->t_max, g.tb_kind == 1 ? 4 : kMaxTemporal);
-    // output rows per wave segment: 24 for kind 4 (12-slot unrolled march),
-    // 40 for kind 5 (4096^2: 6.42 us/sweep vs 6.50 at 32 and 6.68 at 24)
-    g.tb_rows = g.tb_kind == 5 ? 40 : 24;
+    // output rows per wave segment: 24 for kind 4 (12-slot unrolled march);
+    // kind 5 sizes its segments to one round of resident waves (tb_rows 0,
+    // cfd_jacobi_lds.hip lds_segments; 4096^2: ~38 rows, fixed 40 rows gave
+    // 6.42 us/sweep, 32 gave 6.50, 24 gave 6.68)
+    g.tb_rows = g.tb_kind == 5 ? 0 : 24;
     if (const char *rv = getenv("CFD_TB_ROWS")) g.tb_rows = std::max(4, std::min(1024, atoi(rv)));
     g.tb_bpc = 3;
     if (const char *bv = getenv("CFD_TB_BPC")) {   // balanced segmentation instead

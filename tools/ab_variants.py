@@ -20,7 +20,8 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
             sys.exit(1)
         d = json.loads(out.stdout.strip().splitlines()[-1])
         print(json.dumps({"variant": nm, "round": rnd, "us_per_sweep": round(d["us_per_sweep"], 3),
-                          "ms_per_step": round(d["ms_per_step"], 4)}), flush=True)
+                          "ms_per_step": round(d["ms_per_step"], 4),
+                          "state_crc32": d.get("state_crc32")}), flush=True)
         if nm not in best or d["us_per_sweep"] < best[nm]:
             best[nm] = d["us_per_sweep"]
 print(json.dumps({"best_us_per_sweep": best}), flush=True)

@@ -5,6 +5,7 @@ Also the unit rocprofv3 PMC passes attach to.  Usage: tb_one.py [n] [steps]"""
 import json
 import os
 import sys
+import zlib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cfd-demo_amd"))
@@ -19,7 +20,10 @@ m.synchronize()
 m.timing_begin()
 m.update_n(steps)
 tm = m.timing_end()
+st = m.get_state()
+# state checksum: variants of one kernel must agree bit for bit
+crc = zlib.crc32(b"".join(st[k].tobytes() for k in ("u", "v", "p", "p_prime")))
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("CFD_")},
                   "kernel": m.kernel_config, "us_per_sweep": tm["solve_ms"] / tm["sweeps"] * 1e3,
-                  "ms_per_step": tm["step_ms"] / tm["steps"]}), flush=True)
+                  "ms_per_step": tm["step_ms"] / tm["steps"], "state_crc32": crc}), flush=True)
 m.close()
