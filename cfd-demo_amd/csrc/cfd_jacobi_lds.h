@@ -1,0 +1,471 @@
+// cfd_jacobi_lds.h — kind 5: the temporally blocked Jacobi march
+// (model.rs:748-815, T sweeps per launch) with its rhs window in LDS.
+// Included by three translation units that instantiate it for disjoint sets
+// of T (cfd_jacobi_lds.hip: T <= 4 and the dispatch, cfd_jacobi_lds567.hip,
+// cfd_jacobi_lds8.hip), so the kind's compile runs in parallel.
+//
+// Same schedule as the prefetch-pipelined march (cfd_jacobi_pipe.h): a wave
+// owns 64 lanes x 2 columns of a row segment and marches along it; stage s
+// (1..T) of slot v computes row k-s (k = k_first + v) from stage s-1's rows
+// k-s-1..k-s+1, so every stage is one sweep of the reference, bit for bit.
+// What changes is where each value lives between its load and its last use:
+//   PQ[v % PD]  p' input row k+PD, loaded PD slots ahead       (registers)
+//   RQ[v % PD]  rhs row k+PD, loaded PD slots ahead            (registers)
+//   ring[v % D] rhs row k, written at slot v, read by stage s  (LDS, D >= T+1)
+//               at slot v+s
+//   W[s][v % 3] the newest row of stage s                      (registers)
+// The march kind 4 keeps all T+PD rhs rows a slot needs in registers: ~130
+// VGPRs at T = 8, 3 waves per SIMD.  Here the rhs window costs one
+// ds_write_b64 and T ds_read_b64 per slot instead, and the kernel fits 8 waves
+// per SIMD (~60 VGPRs, 4.5 KB of LDS per wave at T = 8).  The slot loop is
+// unrolled by U = D (a multiple of 3 and of PD), so every ring index — W, PQ,
+// RQ and the LDS slot, an immediate offset — is a compile-time constant.
+//
+// The horizontal neighbour sums are written as two scalar adds whose second
+// operand is a DPP lane shift (wave_shr:1 / wave_shl:1): the backend folds
+// each shift into its add (v_add_f32_dpp), one VALU instruction per sum.  This
+// translation unit is built with -fno-slp-vectorize so the two adds are not
+// packed back into a v_pk_add_f32 (VOP3P cannot take DPP); the rest of the
+// update is explicit packed f32 arithmetic on column pairs.
+#pragma once
+#include "cfd_device.h"
+
+namespace cfd {
+namespace {
+
+constexpr int kLdsWaves = 4;   // waves per workgroup (256 threads)
+#ifndef CFD_LDS_SB
+#define CFD_LDS_SB 0   // scheduling barriers: 1 between slots, 2 also between stages
+#endif                 // (bound live ranges; measured no faster, r2 ab_lds_R*.log)
+#ifndef CFD_LDS_PD
+#define CFD_LDS_PD 3   // prefetch distance (slots) of the p' and rhs rows
+#endif
+// CFD_LDS_DIAG (timing diagnostics only, WRONG results): 1 = no global loads
+// (rows are a lane constant), 2 = no LDS ring (stage s reads the register
+// prefetch of another row), 3 = both
+#ifndef CFD_LDS_DIAG
+#define CFD_LDS_DIAG 0
+#endif
+#ifndef CFD_LDS_WPE
+#define CFD_LDS_WPE 0  // > 0: minimum waves per SIMD for the register allocation
+#endif
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// CFD_LDS_STAMP (diagnostic builds only): every wave of a RES=false launch
+// records its start and end (s_memrealtime, 100 MHz), its shader-clock span
+// (s_memtime) and its HW_ID / XCC_ID in g_lds_stamp (vector stores), read back
+// by cfd_diag_lds_stamps.  Off in the product build.
+#ifndef CFD_LDS_PRIO
+#define CFD_LDS_PRIO 1  // progress-ordered issue priority (LdsMarch::set_prio)
+#endif
+#ifndef CFD_LDS_STAMP
+#define CFD_LDS_STAMP 0
+#endif
+#if CFD_LDS_STAMP
+constexpr int kStampWaves = 1 << 15;
+__device__ unsigned long long g_lds_stamp[kStampWaves * 4];
+#endif
+
+#ifndef CFD_LDS_LAG
+#define CFD_LDS_LAG 1  // rows between consecutive stages of one slot (see LdsMarch)
+#endif
+constexpr int lds_gcd(int a, int b) { return b == 0 ? a : lds_gcd(b, a % b); }
+// rhs ring depth: the smallest multiple of lcm(NW, PD) that holds L*T+1 rows
+// (NW = L+2 rows of each stage's register window)
+constexpr int ring_depth(int T, int PD, int L) {
+    const int nw = L + 2;
+    const int q = nw / lds_gcd(nw, PD) * PD;
+    return ((L * T + 1 + q - 1) / q) * q;
+}
+
+template <int T, int FAST, bool RES>
+struct LdsMarch {
+    // Lag L: stage s of slot v computes row k - L*s.  L = 1 is the plain
+    // pipeline (stage s reads stage s-1's row of the SAME slot: one serial
+    // chain of T updates per slot).  L = 2 skews the stages so that stage s
+    // reads only rows stage s-1 finished in EARLIER slots: the T updates of a
+    // slot are independent and the wave has T-way instruction-level
+    // parallelism, for one more row per stage in registers (NW = L+2) and an
+    // rhs window of L*T+1 rows.  The set of (stage, row) updates is the same.
+    static constexpr int L = CFD_LDS_LAG;
+    static constexpr int NW = L + 2;               // register window rows per stage
+    static constexpr int PD = CFD_LDS_PD;          // prefetch distance (slots) of p' and rhs
+    static constexpr int D = ring_depth(T, PD, L); // rhs ring depth; PD and NW divide it
+    static constexpr int U = D;                    // slot unroll: every ring index compile-time
+    static constexpr int WARM = (L + 1) * T;       // stage s starts at slot (L+1)*s
+    static constexpr int H = (T + 1) / 2;          // halo lanes per side (2 columns per lane)
+    static constexpr int OUTL = 64 - 2 * H;        // lanes whose columns are stored
+    static_assert(D % PD == 0 && D % NW == 0 && D >= L * T + 1, "ring geometry");
+    static_assert(L == 1 || L == 2, "lag");
+
+    f2 W[T][NW];
+    f2 PQ[PD];
+    f2 RQ[PD];
+    float2 *ring;        // this wave's D x 64 slots (LDS)
+    int lane;
+    int k_first, S, lo_clamp, hi_clamp, nch, g_first, g_last, g_top, g_zero, row_bytes;
+    int ch, vo_ld, vo_st, abase, dir;
+    bool e0, e1;         // residual columns (kCol slots)
+    const Geom *g;       // the kernel argument: divisors and their reciprocals
+    __amdgpu_buffer_rsrc_t rs_p, rs_r, rs_d;
+    float m;
+
+    __device__ __forceinline__ int act(int vrow) const { return abase + dir * vrow; }
+
+    // Row `vrow` (virtual, march order) of p' or rhs.  Rows outside the
+    // allocation lie beyond the global boundary and rows past the segment's
+    // last input row are never needed: both are clamped to a row that exists
+    // (their values only reach halo rows that the boundary patch overwrites).
+    __device__ __forceinline__ f2 ld(__amdgpu_buffer_rsrc_t rs, int vrow) const {
+        if (CFD_LDS_DIAG & 1) return (f2){__int_as_float(vo_ld + vrow), 1.0f};
+        vrow = vrow < k_first + S ? vrow : k_first + S - 1;
+        int row = act(vrow);
+        row = row < lo_clamp ? lo_clamp : (row > hi_clamp ? hi_clamp : row);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo_ld, (row - lo_clamp) * row_bytes, 0);
+        return (f2){__uint_as_float(v.x), __uint_as_float(v.y)};
+    }
+    __device__ __forceinline__ void st(const f2 &x, int row) const {
+        const u32x2 v = {__float_as_uint(x.x), __float_as_uint(x.y)};
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - lo_clamp) * row_bytes, 0);
+    }
+
+    // One reference update (model.rs:775-793) of the lane's column pair.
+    __device__ __forceinline__ f2 update(const f2 &B, const f2 &C, const f2 &Tp, const f2 &Rh) const {
+        // horizontal: P(i+1) + P(i-1); the neighbour columns come from the
+        // adjacent lanes (left lane's second column, right lane's first)
+        const float hx = C.y + from_left(C.y);
+        const float hy = C.x + from_right(C.x);
+        const f2 h = {hx, hy};
+        const f2 v = Tp + B;
+        const f2 hz = fdiv2<FAST>(h, g->dx_sq, g->r_dx_sq);
+        const f2 vt = fdiv2<FAST>(v, g->dy_sq, g->r_dy_sq);
+        const f2 pu = fdiv2<FAST>(hz + vt - Rh, g->denom, g->r_denom);
+        const float omega = 0.75f;
+        const float om1 = 1.0f - omega;
+        return omega * pu + om1 * C;
+    }
+
+    // E: which boundary logic a slot carries.  kCol: the global column
+    // patches and the residual's column range (waves at the left/right
+    // boundary); kRow: the global row patches and boundary-row stores (waves
+    // whose rows reach a global boundary row).
+    static constexpr int kCol = 1, kRow = 2;
+
+    template <int E>
+    __device__ __forceinline__ f2 stage(const f2 &B, const f2 &C, const f2 &Tp, const f2 &Rh) const {
+        f2 o = update(B, C, Tp, Rh);
+        if (E & kCol) {
+            if (ch == 0) o.x = o.y;             // P(0,j) = P(1,j)
+            if (ch == nch - 1) o.y = 0.0f;      // P(nx-1,j) = 0
+        }
+        return o;
+    }
+
+    // Slot v (k = k_first + v), V_ == v (mod U).  GUARD 0: warm-up (V_ == v,
+    // stage s runs from slot (L+1)s on); GUARD 2: the final partial group.
+    template <int V_, int GUARD, int E>
+    __device__ __forceinline__ void slot(int v) {
+        if (GUARD == 2 && v >= S) return;
+        if (CFD_LDS_SB >= 1) __builtin_amdgcn_sched_barrier(0);
+        const int k = k_first + v;
+        W[0][V_ % NW] = PQ[V_ % PD];                                 // input row k
+        PQ[V_ % PD] = ld(rs_p, k + PD);
+        if (!(CFD_LDS_DIAG & 2))
+            ring[(V_ % D) * 64 + lane] = make_float2(RQ[V_ % PD].x, RQ[V_ % PD].y);   // rhs row k
+        RQ[V_ % PD] = ld(rs_r, k + PD);
+#pragma unroll
+        for (int s = 1; s <= T; ++s) {
+            if (GUARD == 0 && V_ < (L + 1) * s) continue;            // compile-time
+            if (CFD_LDS_SB >= 2 && s > 1) __builtin_amdgcn_sched_barrier(0);
+            const int r = k - L * s;
+            const float2 rh = (CFD_LDS_DIAG & 2)
+                                  ? make_float2(RQ[(V_ + s) % PD].x, RQ[(V_ + s) % PD].y)
+                                  : ring[((V_ - L * s + 8 * D) % D) * 64 + lane];
+            // stage s-1 finished row x at slot x - k_first + L(s-1)
+            constexpr int kW = 4 * NW;
+            const f2 &B = W[s - 1][(V_ - L - 1 + kW) % NW];          // stage s-1, row r-1
+            const f2 &C = W[s - 1][(V_ - L + kW) % NW];              //            row r
+            const f2 &Tp = W[s - 1][(V_ + 1 - L + kW) % NW];         //            row r+1
+            f2 n = stage<E>(B, C, Tp, (f2){rh.x, rh.y});
+            if (s < T) {
+                // stage s's row r-1 is its previous slot's row
+                if ((E & kRow) && r == g_top) n = W[s][(V_ - 1 + kW) % NW]; // P(i,ny-1) = P(i,ny-2)
+                W[s][V_ % NW] = n;
+                if ((E & kRow) && r == g_first) W[s][(V_ - 1 + kW) % NW] = n; // P(i,0) = P(i,1)
+            } else {
+                const int ra = act(r);
+                if (RES && ra >= 0 && ra < nyl_) {
+                    const f2 d = n - C;
+                    if (!(E & kCol)) {
+                        m = fmaxf(fmaxf(m, fabsf(d.x)), fabsf(d.y));
+                    } else {
+                        if (e0) m = fmaxf(m, fabsf(d.x));
+                        if (e1) m = fmaxf(m, fabsf(d.y));
+                    }
+                }
+                st(n, ra);
+                if ((E & kRow) && r == g_first) st(n, g_zero);
+                if ((E & kRow) && r == g_last) st(n, g_top);
+            }
+        }
+    }
+    int nyl_;
+
+    template <int V_, int E>
+    __device__ __forceinline__ void warmup() {
+        if constexpr (V_ < WARM) {
+            slot<V_, 0, E>(V_);
+            warmup<V_ + 1, E>();
+        }
+    }
+
+    template <int J, int GUARD, int E>
+    __device__ __forceinline__ void group(int base) {
+        if constexpr (J < U) {
+            slot<WARM + J, GUARD, E>(base + J);
+            group<J + 1, GUARD, E>(base);
+        }
+    }
+
+    // Issue priority from progress.  The SIMD arbiter issues from the oldest
+    // ready wave, so of the ~4 equal marches sharing a SIMD the first-launched
+    // finishes first and the last one runs its final third nearly alone, at
+    // the latency of its own dependent chain (r2 wave timeline: ends at 21 /
+    // 25 / 32 / 39 us for one 40-row launch).  A wave lowers its priority as
+    // it passes each quarter of its march, so the waves behind catch up and
+    // the SIMD keeps four waves to issue from until close to the end.
+    __device__ __forceinline__ void set_prio(int done) const {
+        if (!CFD_LDS_PRIO) return;
+        const int rows = S - WARM, d4 = 4 * done;   // wave-uniform
+        if (d4 >= 3 * rows)
+            __builtin_amdgcn_s_setprio(0);
+        else if (d4 >= 2 * rows)
+            __builtin_amdgcn_s_setprio(1);
+        else if (d4 >= rows)
+            __builtin_amdgcn_s_setprio(2);
+        else
+            __builtin_amdgcn_s_setprio(3);
+    }
+
+    // E: 0 (interior waves), kCol (waves at the left/right boundary), or
+    // kCol|kRow (waves whose rows reach a global boundary row; the column
+    // patches are no-ops on interior columns).  Chosen once per wave: a
+    // per-group switch between paths costs ~15 VGPRs of phi copies.
+    template <int E>
+    __device__ __forceinline__ void run() {
+        set_prio(0);
+        warmup<0, E>();
+        int base = WARM;
+        const int full_end = WARM + ((S - WARM) / U) * U;
+        for (; base < full_end; base += U) {
+            set_prio(base - WARM);
+            group<0, 1, E>(base);
+        }
+        set_prio(base - WARM);
+        if (base < S) group<0, 2, E>(base);
+    }
+};
+
+#if CFD_LDS_WPE > 0
+#define CFD_LDS_BOUNDS __launch_bounds__(kLdsWaves * 64, CFD_LDS_WPE)
+#else
+#define CFD_LDS_BOUNDS __launch_bounds__(kLdsWaves * 64)
+#endif
+template <int T, int FAST, bool RES>
+__global__ CFD_LDS_BOUNDS void k_jacobi_lds(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
+    int wlo, int whi) {
+    using M = LdsMarch<T, FAST, RES>;
+    __shared__ float2 lds[kLdsWaves * M::D * 64];
+#if CFD_LDS_STAMP
+    const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+    struct StampOnExit {
+        unsigned long long rt0, t0;
+        __device__ ~StampOnExit() {
+            if (RES) return;
+            const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            // hwreg(id, 0, 32): HW_ID = 4, XCC_ID = 20
+            const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+            const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+            const int idx = (int)blockIdx.x * kLdsWaves + ((int)threadIdx.x >> 6);
+            if ((threadIdx.x & 63) == 0 && idx < kStampWaves) {
+                g_lds_stamp[idx * 4 + 0] = rt0;
+                g_lds_stamp[idx * 4 + 1] = rt1;
+                g_lds_stamp[idx * 4 + 2] = t1 - t0;
+                g_lds_stamp[idx * 4 + 3] = ((unsigned long long)xcc << 32) | hw;
+            }
+        }
+    } stamp_guard{st_rt0, st_t0};
+#endif
+    if (pass_off(ctl, pass)) return;
+    M w;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int lane = (int)threadIdx.x & 63;
+    const int bid = xcd_block(g);
+    const int wc = bid % nwc;
+    const int seg = (bid / nwc) * kLdsWaves + wave;
+    const int nrows = out_hi - out_lo;
+    if (seg >= nseg) return;
+    // rows split in proportion to weights: 16 per segment, wlo / whi for the
+    // first / last one (lighter where that segment runs the boundary-row path)
+    const long total = nseg == 1 ? 16 : wlo + whi + 16L * (nseg - 2);
+    auto cum = [&](int i) -> long { return i <= 0 ? 0 : (i >= nseg ? total : wlo + 16L * (i - 1)); };
+    const int r0 = out_lo + (int)(cum(seg) * nrows / total);
+    const int r1 = out_lo + (int)(cum(seg + 1) * nrows / total);
+    if (r0 >= r1) return;
+    const int nx = g.nx;
+    w.ring = lds + wave * M::D * 64;
+    w.lane = lane;
+    w.nch = nx / 2;
+    w.nyl_ = g.nyl;
+    w.lo_clamp = -g.hg;
+    w.hi_clamp = g.nyl + g.hg - 1;
+    w.ch = wc * M::OUTL - M::H + lane;
+    const bool in_dom = w.ch >= 0 && w.ch < w.nch;
+    const bool out_lane = in_dom && lane >= M::H && lane < 64 - M::H;
+    const int col = 2 * w.ch;
+    w.row_bytes = nx * 4;
+    constexpr int kFar = 0x7FFF0000;   // voffset of a lane that must not touch memory
+    w.vo_ld = in_dom ? col * 4 : kFar;
+    w.vo_st = out_lane ? col * 4 : kFar;
+    // buffers ping-pong once per LAUNCH: par = launches since the solve began
+    const int si = (ctl->cur + par) & 1;
+    float *src_alloc = si ? pb : pa;
+    float *dst_alloc = si ? pa : pb;
+    const int pbytes = (g.nyl + 2 * g.hg) * nx * 4;
+    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
+    w.rs_d = __builtin_amdgcn_make_buffer_rsrc(dst_alloc, 0, pbytes, 0x00020000);
+    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)g.hg * nx), 0, pbytes,
+                                               0x00020000);
+    w.g = &g;
+    // residual columns 1..=nx-8 (the reference's full 8-lane chunks, Q6)
+    w.e0 = out_lane && col >= 1 && col <= nx - 8;
+    w.e1 = out_lane && col + 1 >= 1 && col + 1 <= nx - 8;
+    w.g_first = 1 - g.j0;
+    w.g_last = g.ny - 2 - g.j0;
+    w.g_top = g.ny - 1 - g.j0;
+    w.g_zero = -g.j0;
+    w.m = 0.0f;
+    w.k_first = r0 - T;
+    w.S = (r1 - r0) + M::WARM;
+    w.abase = 0;
+    w.dir = 1;
+    const f2 z = {0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < T; ++s)
+#pragma unroll
+        for (int q = 0; q < M::NW; ++q) w.W[s][q] = z;
+    // edge waves: a lane stores column 0 or a column outside the residual
+    // range, or a stage touches a global boundary row; interior waves skip
+    // all boundary logic
+    const int ch_lo = wc * M::OUTL - M::H, ch_hi = ch_lo + 63;
+    const bool col_edge = ch_lo <= 0 || 2 * (ch_hi + 1) > nx - 8;
+    const int lo_row = w.k_first - 2, hi_row = r1 + M::L * T + 2;   // every row a stage computes
+    auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
+    const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
+    const bool edge = col_edge || row_edge;
+    // odd interior segments march downward through the mirrored rows (the
+    // stencil is symmetric and f32 addition commutative: same bits), so
+    // neighbouring segments read their shared rows at the same time
+    if (!edge && (seg & 1)) {
+        w.abase = r0 + r1 - 1;
+        w.dir = -1;
+    }
+#pragma unroll
+    for (int q = 0; q < M::PD; ++q) {
+        w.PQ[q] = w.ld(w.rs_p, w.k_first + q);
+        w.RQ[q] = w.ld(w.rs_r, w.k_first + q);
+    }
+    if (row_edge)
+        w.template run<M::kCol | M::kRow>();
+    else if (col_edge)
+        w.template run<M::kCol>();
+    else
+        w.template run<0>();
+    if (!RES) return;
+    const float m = wave_max(out_lane ? w.m : 0.0f);
+    if (lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, m);
+}
+
+// Workgroups of k_jacobi_lds<T, FAST, RES> one CU holds at once (occupancy
+// API, cached per instantiation).
+template <int T, int FAST, bool RES>
+int lds_blocks_per_cu() {
+    static const int nb = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &n, reinterpret_cast<const void *>(&k_jacobi_lds<T, FAST, RES>), kLdsWaves * 64, 0) !=
+                hipSuccess ||
+            n < 1)
+            n = 1;
+        return n;
+    }();
+    return nb;
+}
+
+// Segments per wave column.  g.tb_rows > 0: fixed rows per segment.  0
+// (default): as many segments as ONE round of resident waves holds — every
+// SIMD gets its waves at once and the same march length, so no CU waits for a
+// second, partial round — or whole multiples of a round when a round would
+// make segments longer than kMaxRows.
+template <int T, int FAST, bool RES>
+int lds_segments(const Geom &g, int nrows, int nwc) {
+    if (g.tb_rows > 0) return cdiv(nrows, g.tb_rows);
+    constexpr int kMaxRows = 160, kMinRows = 8;
+    const int wgs_per_col = std::max(1, g.n_cu * lds_blocks_per_cu<T, FAST, RES>() / nwc);
+    const int per_round = kLdsWaves * wgs_per_col;
+    const int rounds = std::max(1, cdiv(nrows, (long)per_round * kMaxRows));
+    return std::max(1, std::min(per_round * rounds, nrows / kMinRows));
+}
+
+template <int T, bool RES>
+void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+                  uint32_t *rs, hipStream_t s) {
+    const int nch = g.nx / 2;
+    const int nwc = cdiv(nch, LdsMarch<T, 1, RES>::OUTL);
+    const int nrows = out_hi - out_lo;
+    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, RES>(g, nrows, nwc)
+                     : g.fastdiv == 2 ? lds_segments<T, 2, RES>(g, nrows, nwc)
+                                      : lds_segments<T, 0, RES>(g, nrows, nwc);
+    const dim3 grid(nwc * cdiv(nseg, kLdsWaves)), block(kLdsWaves * 64);
+    float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
+    // a segment whose rows reach a global boundary row runs the kCol|kRow
+    // path, ~1.45x the VALU work per row of an interior one (r2 wave
+    // timeline): it gets ~1/1.45 of the rows
+    constexpr int kEdgeWeight = 11;
+    const int reach = T + 2;
+    const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
+    const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
+#define CFD_LDS_LAUNCH(FASTV)                                                                      \
+    hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, RES>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, \
+                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi)
+    if (g.fastdiv == 1)
+        CFD_LDS_LAUNCH(1);
+    else if (g.fastdiv == 2)
+        CFD_LDS_LAUNCH(2);
+    else
+        CFD_LDS_LAUNCH(0);
+#undef CFD_LDS_LAUNCH
+}
+
+// T sweeps per launch, with (rs != nullptr) or without the residual.
+template <int T>
+void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+                  uint32_t *rs, hipStream_t s) {
+    if (rs)
+        launch_lds_t<T, true>(g, f, pass, par, out_lo, out_hi, rs, s);
+    else
+        launch_lds_t<T, false>(g, f, pass, par, out_lo, out_hi, rs, s);
+}
+
+}  // namespace
+
+// per-translation-unit entry points (cfd_jacobi_lds*.hip)
+void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int out_lo,
+                     int out_hi, uint32_t *rs, hipStream_t s);
+void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+                   uint32_t *rs, hipStream_t s);
+
+}  // namespace cfd
