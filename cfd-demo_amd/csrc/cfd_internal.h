@@ -89,6 +89,7 @@ struct Geom {
     // are exact powers of two (then sdiv multiplies, bit-identically)
     float r_dx, r_dy, r_dxx, r_dyy;
     int32_t sp_pow2;
+    int32_t pred_div;     // 1: fused predictors + divergence (k_predict_div) where it applies
 };
 
 struct Fields {
@@ -118,6 +119,10 @@ void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipSt
 void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 // u and v predictors in one pass (same results as the two launches above).
 void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+// first-order predictors + divergence in one row march (k_predict_div), when
+// predict_div_fused(): replaces launch_predict + the step's first divergence
+bool predict_div_fused(const Geom &g, const Fields &f);
+void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s);
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).

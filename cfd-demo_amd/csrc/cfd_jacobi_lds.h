@@ -57,6 +57,9 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #ifndef CFD_LDS_PRIO
 #define CFD_LDS_PRIO 1  // progress-ordered issue priority (LdsMarch::set_prio)
 #endif
+#ifndef CFD_LDS_COMPACT
+#define CFD_LDS_COMPACT 0  // 1: warm-up and tail share one run-time-guarded slot group
+#endif
 #ifndef CFD_LDS_STAMP
 #define CFD_LDS_STAMP 0
 #endif
@@ -161,10 +164,11 @@ struct LdsMarch {
     }
 
     // Slot v (k = k_first + v), V_ == v (mod U).  GUARD 0: warm-up (V_ == v,
-    // stage s runs from slot (L+1)s on); GUARD 2: the final partial group.
+    // stage s runs from slot (L+1)s on); GUARD 2: the final partial group;
+    // GUARD 3: both, decided at run time (CFD_LDS_COMPACT).
     template <int V_, int GUARD, int E>
     __device__ __forceinline__ void slot(int v) {
-        if (GUARD == 2 && v >= S) return;
+        if ((GUARD == 2 || GUARD == 3) && v >= S) return;
         if (CFD_LDS_SB >= 1) __builtin_amdgcn_sched_barrier(0);
         const int k = k_first + v;
         W[0][V_ % NW] = PQ[V_ % PD];                                 // input row k
@@ -175,6 +179,7 @@ struct LdsMarch {
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
             if (GUARD == 0 && V_ < (L + 1) * s) continue;            // compile-time
+            if (GUARD == 3 && v < (L + 1) * s) continue;             // wave-uniform
             if (CFD_LDS_SB >= 2 && s > 1) __builtin_amdgcn_sched_barrier(0);
             const int r = k - L * s;
             const float2 rh = (CFD_LDS_DIAG & 2)
@@ -218,11 +223,12 @@ struct LdsMarch {
         }
     }
 
-    template <int J, int GUARD, int E>
+    // U slots from `base`; OFF == base (mod U)
+    template <int J, int GUARD, int E, int OFF = WARM>
     __device__ __forceinline__ void group(int base) {
         if constexpr (J < U) {
-            slot<WARM + J, GUARD, E>(base + J);
-            group<J + 1, GUARD, E>(base);
+            slot<OFF + J, GUARD, E>(base + J);
+            group<J + 1, GUARD, E, OFF>(base);
         }
     }
 
@@ -252,6 +258,22 @@ struct LdsMarch {
     // per-group switch between paths costs ~15 VGPRs of phi copies.
     template <int E>
     __device__ __forceinline__ void run() {
+        if (CFD_LDS_COMPACT) {
+            // warm-up and tail through one run-time-guarded group: half the
+            // code of the unrolled warm-up + guarded tail (2U >= WARM)
+            static_assert(2 * U >= WARM, "warm-up fits two groups");
+            set_prio(0);
+            group<0, 3, E, 0>(0);
+            group<0, 3, E, 0>(U);
+            int base = 2 * U;
+            for (; base + U <= S; base += U) {
+                set_prio(base - WARM);
+                group<0, 1, E, 0>(base);
+            }
+            set_prio(base - WARM);
+            if (base < S) group<0, 3, E, 0>(base);
+            return;
+        }
         set_prio(0);
         warmup<0, E>();
         int base = WARM;

@@ -475,6 +475,149 @@ __global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pas
     *reinterpret_cast<float4 *>(f.rhs + (long)lj * nx + i0) = r;
 }
 
+// ------------------------------------------- predict + divergence (K1-K3)
+
+// Both first-order predictors and the divergence in one pass (piso_step
+// K1-K3: model.rs:538-670 and :1406-1440), over k_predict4r's tile: a lane
+// owns 4 columns (i0 = 4c) and RPT rows lj0..lj0+RPT-1.  Besides u* and v* of
+// those rows it predicts v* of row lj0 (the tile below owns it) and takes the
+// east face u*(r, i0+4) from the lane on its right (DPP lane shift), so rhs
+// of its own cells needs no u* / v* from memory: the divergence's re-read of
+// u*, v* (8 B per cell) and a launch go, for one more v row in the window
+// (RPT+3 rows of v, RPT+2 of u) and 1/RPT more v* arithmetic.  Lane 63 only
+// feeds lane 62's east face, so waves step 63 chunks.  Faces the reference
+// does not predict (face 0, column 0 of v, rows outside glo..u_hi / v_hi) take
+// u* / v* from memory, as k_divergence reads them.  The arithmetic is
+// u_pred_val / v_pred_val and k_divergence's, bit for bit.
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+
+struct RAcc3 {   // stencil rows dj = -1, 0, +1 of u and of v, column q of four
+    const float *u0, *u1, *u2, *v0, *v1, *v2;
+    int q;
+    __device__ __forceinline__ float U(int di, int dj) const {
+        return (dj < 0 ? u0 : (dj == 0 ? u1 : u2))[q + 1 + di];
+    }
+    __device__ __forceinline__ float V(int di, int dj) const {
+        return (dj < 0 ? v0 : (dj == 0 ? v1 : v2))[q + 1 + di];
+    }
+};
+
+template <int SP, int RPT>
+__global__ __launch_bounds__(kBlock) void k_predict_div(Geom g, Fields f, float dt_override,
+                                                        int glo, int u_hi, int v_hi, int nwc,
+                                                        int ntile) {
+    const int nx = g.nx, W = nx + 1;
+    const int bid = xcd_block(g);
+    const int lane = (int)threadIdx.x & 63;
+    const int wc = bid % nwc;
+    const int tile = (bid / nwc) * (kBlock / 64) + ((int)threadIdx.x >> 6);
+    if (tile >= ntile) return;   // wave-uniform
+    const int lj0 = tile * RPT;
+    const int c = wc * 63 + lane;
+    const bool live = 4 * c < nx;
+    const bool out = live && lane < 63;     // lanes that store
+    const int i0 = live ? 4 * c : nx - 4;   // dead lanes compute on safe columns
+    const int u_cap = u_hi + 1 > v_hi ? u_hi + 1 : v_hi;   // last u row any face reads
+    const int v_cap = v_hi + 1;                            // last v row any face reads
+    const float dt = dt_of(f.ctl, dt_override);
+    const float rdx = g.r_dx, rdy = g.r_dy, dx = g.dx, dy = g.dy;
+    // ur[k] = u row lj0-1+k, vr[k] = v row lj0-1+k; columns i0-1..i0+4
+    float ur[RPT + 2][6], vr[RPT + 3][6];
+#pragma unroll
+    for (int k = 0; k < RPT + 2; ++k) {
+        const int r = min(max(lj0 - 1 + k, glo - 1), u_cap);
+        const float *p = f.u + (long)r * W + i0;
+        ur[k][0] = i0 > 0 ? p[-1] : 0.0f;
+        const f4u a = *reinterpret_cast<const f4u *>(p);
+        ur[k][1] = a.x; ur[k][2] = a.y; ur[k][3] = a.z; ur[k][4] = a.w;
+        ur[k][5] = p[4];
+    }
+#pragma unroll
+    for (int k = 0; k < RPT + 3; ++k) {
+        const int r = min(max(lj0 - 1 + k, glo - 1), v_cap);
+        const float *p = f.v + (long)r * nx + i0;
+        vr[k][0] = i0 > 0 ? p[-1] : 0.0f;
+        const float4 a = *reinterpret_cast<const float4 *>(p);
+        vr[k][1] = a.x; vr[k][2] = a.y; vr[k][3] = a.z; vr[k][4] = a.w;
+        // column nx wraps to the next row's column 0 (flat index): only the
+        // stencil's middle row (<= v_hi) needs it, and row v_hi + 1 exists
+        vr[k][5] = (i0 + 4 < nx || r <= v_hi) ? p[4] : 0.0f;
+    }
+    const int r_end = min(lj0 + RPT, g.nyl);   // rhs rows lj0..r_end-1
+    // v* rows lj0..lj0+RPT
+    float vs[RPT + 1][4];
+#pragma unroll
+    for (int k = 0; k <= RPT; ++k) {
+        const int rr = lj0 + k;
+        if (rr >= glo && rr <= v_hi) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                vs[k][q] = v_pred_val<0, SP>(g, f, dt_override, i0 + q, rr,
+                                             RAcc3{ur[k + 1], ur[k + 1], ur[k + 1], vr[k], vr[k + 1],
+                                                   vr[k + 2], q});
+            if (i0 == 0) vs[k][0] = f.v_star[(long)rr * nx];   // column 0 is not predicted
+            // own rows lj0+1..r_end, and row lj0 of the lowest tile
+            if (out && (k > 0 || lj0 == 0) && rr <= r_end) {
+                float *d = f.v_star + (long)rr * nx + i0;
+                if (i0 > 0) {
+                    *reinterpret_cast<float4 *>(d) = make_float4(vs[k][0], vs[k][1], vs[k][2], vs[k][3]);
+                } else {
+                    d[1] = vs[k][1];
+                    d[2] = vs[k][2];
+                    d[3] = vs[k][3];
+                }
+            }
+        } else if (rr <= r_end) {
+            const float4 a = *reinterpret_cast<const float4 *>(f.v_star + (long)rr * nx + i0);
+            vs[k][0] = a.x; vs[k][1] = a.y; vs[k][2] = a.z; vs[k][3] = a.w;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int r = lj0 + k;
+        if (r >= r_end) break;   // wave-uniform
+        float us[4];
+        const bool upred = r >= glo && r <= u_hi;
+        const long ku = (long)r * W + i0;
+        if (upred) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                us[q] = u_pred_val<0, SP>(g, f, dt_override, i0 + q, r,
+                                          RAcc3{ur[k], ur[k + 1], ur[k + 2], vr[k], vr[k + 1],
+                                                vr[k + 2], q});
+            if (i0 == 0) us[0] = f.u_star[ku];   // face 0 is not predicted
+        } else {
+            const f4u a = *reinterpret_cast<const f4u *>(f.u_star + ku);
+            us[0] = a.x; us[1] = a.y; us[2] = a.z; us[3] = a.w;
+        }
+        float east = from_right(us[0]);
+        if (i0 + 4 == nx) {
+            if (upred) {
+                const GAcc a{f.u, f.v, ku + 4, (long)r * nx + i0 + 4, W, nx};
+                east = u_pred_val<0, SP>(g, f, dt_override, nx, r, a);
+            } else {
+                east = f.u_star[ku + 4];
+            }
+        }
+        if (out) {
+            if (upred) {
+                float *d = f.u_star + ku;
+                if (i0 > 0) d[0] = us[0];
+                d[1] = us[1];
+                d[2] = us[2];
+                d[3] = us[3];
+                if (i0 + 4 == nx) d[4] = east;
+            }
+            float4 rh;
+            rh.x = (sdiv<SP>(us[1] - us[0], dx, rdx) + sdiv<SP>(vs[k + 1][0] - vs[k][0], dy, rdy)) / dt;
+            rh.y = (sdiv<SP>(us[2] - us[1], dx, rdx) + sdiv<SP>(vs[k + 1][1] - vs[k][1], dy, rdy)) / dt;
+            rh.z = (sdiv<SP>(us[3] - us[2], dx, rdx) + sdiv<SP>(vs[k + 1][2] - vs[k][2], dy, rdy)) / dt;
+            rh.w = (sdiv<SP>(east - us[3], dx, rdx) + sdiv<SP>(vs[k + 1][3] - vs[k][3], dy, rdy)) / dt;
+            *reinterpret_cast<float4 *>(f.rhs + (long)r * nx + i0) = rh;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- Jacobi (K4)
 
 // One weighted-Jacobi sweep (omega 0.75) with the p' boundary conditions
@@ -959,7 +1102,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
             du = fmaxf(fmaxf(fmaxf(du, fabsf(n0 - o0)), fmaxf(fabsf(n1 - o1), fabsf(n2 - o2))),
                        fabsf(n3 - o3));
             mu = fmaxf(fmaxf(fmaxf(mu, fabsf(n0)), fmaxf(fabsf(n1), fabsf(n2))), fabsf(n3));
-            bad |= nonfinite(n0) | nonfinite(n1) | nonfinite(n2) | nonfinite(n3);
+            bad |= nonfinite(n0) || nonfinite(n1) || nonfinite(n2) || nonfinite(n3);
             if (i0 + 4 == nx) {   // outflow face nx copies the corrected face nx-1 (Q9)
                 float n4 = cf_u_face<SP>(g, inlet, dt, nx, j, s3, pc.w, pc.z);
                 if (f.n_obs > 0 && (f.mask_u[k + 4] & 2)) n4 = 0.0f;
@@ -990,7 +1133,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
         dv = fmaxf(fmaxf(fmaxf(dv, fabsf(nv.x - ov.x)), fmaxf(fabsf(nv.y - ov.y), fabsf(nv.z - ov.z))),
                    fabsf(nv.w - ov.w));
         mv = fmaxf(fmaxf(fmaxf(mv, fabsf(nv.x)), fmaxf(fabsf(nv.y), fabsf(nv.z))), fabsf(nv.w));
-        bad |= nonfinite(nv.x) | nonfinite(nv.y) | nonfinite(nv.z) | nonfinite(nv.w);
+        bad |= nonfinite(nv.x) || nonfinite(nv.y) || nonfinite(nv.z) || nonfinite(nv.w);
         if (lj < g.nyl) {
             float4 p = *reinterpret_cast<const float4 *>(f.p + rp);
             p.x = p.x + pc.x;
@@ -1200,6 +1343,34 @@ void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream
         if (g.sp_pow2) CFD_LAUNCH_P(1, 1); else CFD_LAUNCH_P(1, 0);
     }
 #undef CFD_LAUNCH_P
+}
+
+bool predict_div_fused(const Geom &g, const Fields &f) {
+    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    return g.pred_div && g.scheme == 0 && g.nx % 4 == 0 && g.nx >= 8 && a16(f.v) && a16(f.v_star) &&
+           a16(f.rhs);
+}
+
+void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+    const int glo = (g.j0 > 1 ? g.j0 : 1) - g.j0;
+    const int u_hi = ((g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2)) - g.j0;
+    const int v_hi = ((g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1)) - g.j0;
+    static const int rpt = [] {
+        const char *e = getenv("CFD_PRED_DIV_RPT");
+        return e && atoi(e) == 4 ? 4 : 2;
+    }();
+    const int nwc = cdiv(g.nx / 4, 63);
+    const int ntile = cdiv(g.nyl, rpt);
+    const dim3 grid(nwc * cdiv(ntile, kBlock / 64));
+#define CFD_LAUNCH_PD(SPV, R)                                                                    \
+    hipLaunchKernelGGL((k_predict_div<SPV, R>), grid, dim3(kBlock), 0, s, g, f, dt_override, glo, \
+                       u_hi, v_hi, nwc, ntile)
+    if (rpt == 4) {
+        if (g.sp_pow2) CFD_LAUNCH_PD(1, 4); else CFD_LAUNCH_PD(0, 4);
+    } else {
+        if (g.sp_pow2) CFD_LAUNCH_PD(1, 2); else CFD_LAUNCH_PD(0, 2);
+    }
+#undef CFD_LAUNCH_PD
 }
 
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,

@@ -643,9 +643,17 @@ struct cfd_model {
     // finish = inside update() with no extra corrector passes: the corrector,
     // the boundaries and the step reductions run as one fused pass.
     int enqueue_piso(float dt_override, bool finish = false) {
-        launch_predict(g, f, dt_override, stream);
+        // K1-K3: the fused march when it applies, else predictors + divergence
+        const bool fused = predict_div_fused(g, f);
+        if (fused)
+            launch_predict_div(g, f, dt_override, stream);
+        else
+            launch_predict(g, f, dt_override, stream);
+        auto first_divergence = [&](int pass) {
+            if (!fused) launch_divergence(g, f, pass, dt_override, stream);
+        };
         if (finish) {
-            launch_divergence(g, f, host_driven() ? -1 : 0, dt_override, stream);
+            first_divergence(host_driven() ? -1 : 0);
             int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
             if (rc) return rc;
             launch_correct_finish(g, f, dt_override, stream);
@@ -653,7 +661,7 @@ struct cfd_model {
             return 0;
         }
         if (!host_driven()) {
-            launch_divergence(g, f, 0, dt_override, stream);
+            first_divergence(0);
             int rc = enqueue_solve(0);
             if (rc) return rc;
             launch_corrector(g, f, 0, dt_override, stream);
@@ -665,7 +673,7 @@ struct cfd_model {
                 launch_corrector(g, f, pass, dt_override, stream);
             }
         } else {
-            launch_divergence(g, f, -1, dt_override, stream);
+            first_divergence(-1);
             float res = 0.f;
             int rc = enqueue_solve_host_driven(&res);
             if (rc) return rc;
@@ -900,11 +908,14 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // Default Jacobi march (measured at 4096^2 on developed fields, r2:
     // profiles/r2/tune_r2b_kind5.log, ab_lds_*.log): with the proven-exact
     // reciprocal multiply, kind 5 (rhs window in LDS, DPP-folded sums) at
-    // T = 8 sweeps per launch and 40-row segments, 6.42 us per sweep, against
-    // 7.75 for kind 4 at T = 8 and 9.04 at T = 4; under IEEE (or FMA-corrected)
+    // T = 8 sweeps per launch, one round of balanced segments, progress-ordered
+    // issue priority and lighter boundary-row segments, 5.1-5.4 us per sweep
+    // (box to box), against 7.75 for kind 4 at T = 8 and 9.04 at T = 4; under IEEE (or FMA-corrected)
     // division the march is VALU-bound and kind 4 at T = 4 stays (r1: 6144^2
     // 7.3e11 vs 6.1e11 cell-updates/s at T = 8).  Single domain and slabs alike.
     g.tb_kind = g.fastdiv == 1 ? 5 : 4;
+    g.pred_div = 1;
+    if (const char *e = getenv("CFD_PRED_DIV")) g.pred_div = atoi(e) != 0;
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
         g.tb_kind = (k == 3 || k == 4 || k == 5) ? k : 1;

@@ -10,25 +10,39 @@ import tempfile
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def code_object(path, tmp):
+def code_objects(path, tmp):
+    """Device code objects in FILE: a .so holds one offload bundle per
+    translation unit, concatenated in .hip_fatbin."""
     fb = os.path.join(tmp, "fatbin")
     subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, fb],
                    check=True)
-    dev = os.path.join(tmp, "dev.o")
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={dev}"], check=True)
-    return dev
+    data = open(fb, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    out = []
+    for i, st in enumerate(starts):
+        part = os.path.join(tmp, f"b{i}")
+        with open(part, "wb") as f:
+            f.write(data[st: starts[i + 1] if i + 1 < len(starts) else len(data)])
+        dev = os.path.join(tmp, f"dev{i}.o")
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={dev}"],
+                           capture_output=True)
+        if r.returncode == 0 and os.path.getsize(dev) > 0:
+            out.append(dev)
+    return out
 
 
 def main():
     path = sys.argv[1]
     pat = re.compile(sys.argv[2] if len(sys.argv) > 2 else ".")
+    notes = syms = ""
     with tempfile.TemporaryDirectory() as tmp:
-        dev = code_object(path, tmp)
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", dev], capture_output=True,
-                               text=True).stdout
-        syms = subprocess.run([f"{LLVM}/llvm-readelf", "-s", "--wide", dev], capture_output=True,
-                              text=True).stdout
+        for dev in code_objects(path, tmp):
+            notes += subprocess.run([f"{LLVM}/llvm-readelf", "--notes", dev], capture_output=True,
+                                    text=True).stdout
+            syms += subprocess.run([f"{LLVM}/llvm-readelf", "-s", "--wide", dev], capture_output=True,
+                                   text=True).stdout
     size = {}
     for line in syms.splitlines():
         f = line.split()
