@@ -89,7 +89,9 @@ struct Geom {
     // are exact powers of two (then sdiv multiplies, bit-identically)
     float r_dx, r_dy, r_dxx, r_dyy;
     int32_t sp_pow2;
-    int32_t pred_div;     // 1: fused predictors + divergence (k_predict_div) where it applies
+    int32_t pred_div;     // predictors + divergence: 2: one row march (k_predict_march, both
+                          // schemes), 1: fused 2-row tile (k_predict_div, first order),
+                          // 0: separate launches; where the fused forms apply
 };
 
 struct Fields {
@@ -123,6 +125,10 @@ void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream
 // predict_div_fused(): replaces launch_predict + the step's first divergence
 bool predict_div_fused(const Geom &g, const Fields &f);
 void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+// both schemes' predictors + divergence in one row march (cfd_predict_march.hip),
+// when predict_march_ok(): replaces launch_predict + the step's first divergence
+bool predict_march_ok(const Geom &g, const Fields &f);
+void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s);
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).

@@ -9,6 +9,7 @@
 //
 // Citations are /root/reference/src/model.rs line numbers.
 #include "cfd_device.h"
+#include "cfd_predict.h"
 
 namespace cfd {
 
@@ -78,85 +79,8 @@ __global__ __launch_bounds__(kBlock) void k_copy_star(Fields f, int pass) {
     copy4(f.v_star_base, f.v_alloc_base, f.v_alloc / 4, tid, stride);
 }
 
-// Stencil access for the predictors: U(di, dj) / V(di, dj) are the u / v
-// values at flat offset (di, dj) from the cell — flat row-major indexing, so
-// the reference's wrap-around reads across row ends (U(nx+1, j) == U(0, j+1))
-// come out as they do in model.rs.
-struct GAcc {
-    const float *u, *v;
-    long c, cv;
-    int W, nx;
-    __device__ __forceinline__ float U(int di, int dj) const { return u[c + di + (long)dj * W]; }
-    __device__ __forceinline__ float V(int di, int dj) const { return v[cv + di + (long)dj * nx]; }
-};
+// Predictor face arithmetic (u_pred_val / v_pred_val) and GAcc: cfd_predict.h.
 
-// ---------------------------------------------------------- u predictor (K1)
-
-// u* on global rows 1..=ny-2, faces 1..=nx (model.rs:538-580 + compute_ustar
-// :382-436).  One thread per face; neighbour reuse comes from L1/L2.  Flux
-// velocities are the raw v values (get_v_north/south :1056-1069).
-template <int SCHEME, int SP, class A>
-__device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, float dt_override,
-                                            int i, int lj, const A &a) {
-    const int nx = g.nx, ny = g.ny, W = nx + 1;
-    const int j = g.j0 + lj;
-    const float uc = a.U(0, 0), ue1 = a.U(1, 0), uw1 = a.U(-1, 0), un1 = a.U(0, 1), us1 = a.U(0, -1);
-    const float vn = a.V(0, 1), vs = a.V(0, 0);
-    float ue, uw, un, us;
-    if (SCHEME == 0) {
-        // u_face_{e,w,n,s}_first_order (:893-908, :929-941, :966-981, :1011-1026)
-        ue = ((uc + ue1) * 0.5f >= 0.0f) ? uc : ue1;
-        uw = ((uw1 + uc) * 0.5f >= 0.0f) ? uw1 : uc;
-        un = (vn >= 0.0f) ? uc : un1;
-        us = (vs >= 0.0f) ? us1 : uc;
-    } else {
-        const size_t ulen = (size_t)W * (size_t)ny;
-        // u_face_e_second_order (:911-926)
-        if (uc >= 0.0f) {
-            ue = (i > 1) ? 1.5f * uc - 0.5f * a.U(-1, 0) : uc;
-        } else if (((size_t)(i + 1) + (size_t)j * W) + 1 < ulen && i < nx - 1) {
-            ue = 1.5f * ue1 - 0.5f * a.U(2, 0);
-        } else {
-            ue = ue1;
-        }
-        // u_face_w_second_order (:944-963)
-        if (uw1 >= 0.0f) {
-            uw = (i > 2) ? 1.5f * uw1 - 0.5f * a.U(-2, 0) : uw1;
-        } else {
-            uw = (i < nx) ? 1.5f * uc - 0.5f * ue1 : uc;
-        }
-        // u_face_n_second_order (:992-1008), decision on averaged v (:983-989)
-        const float vnb = 0.5f * (a.V(-1, 1) + a.V(0, 1));
-        if (vnb >= 0.0f) {
-            un = (j > 1) ? 1.5f * uc - 0.5f * us1 : uc;
-        } else if ((size_t)i + (size_t)(j + 2) * W < ulen && j < ny - 1) {
-            un = 1.5f * un1 - 0.5f * a.U(0, 2);
-        } else {
-            un = un1;
-        }
-        // u_face_s_second_order (:1037-1053), decision on averaged v (:1028-1034)
-        const float vsb = 0.5f * (a.V(-1, 0) + a.V(0, 0));
-        if (vsb >= 0.0f) {
-            us = (j > 1) ? 1.5f * us1 - 0.5f * a.U(0, -2) : us1;
-        } else if (j < ny) {
-            us = 1.5f * uc - 0.5f * un1;
-        } else {
-            us = uc;
-        }
-    }
-    const float dx = g.dx, dy = g.dy, nu = g.nu;
-    const float dt = dt_of(f.ctl, dt_override);
-    const float f_e = ue * ue;
-    const float f_w = uw * uw;
-    const float f_n = vn * un;
-    const float f_s = vs * us;
-    const float convective = sdiv<SP>(f_e - f_w, dx, g.r_dx) + sdiv<SP>(f_n - f_s, dy, g.r_dy);
-    const float laplace = sdiv<SP>(ue1 - 2.0f * uc + uw1, dx * dx, g.r_dxx) +
-                          sdiv<SP>(un1 - 2.0f * uc + us1, dy * dy, g.r_dyy);
-    float r = uc + dt * (-convective + nu * laplace);
-    if (f.any_pmask && (f.mask_u[(long)lj * W + i] & 1)) r = 0.0f;
-    return r;
-}
 
 template <int SCHEME, int SP>
 __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float dt_override,
@@ -166,85 +90,9 @@ __global__ __launch_bounds__(kBlock) void k_u_predictor(Geom g, Fields f, float 
     const int lj = row_lo + bid / nbx;
     if (i > g.nx) return;
     const GAcc a{f.u, f.v, (long)lj * (g.nx + 1) + i, (long)lj * g.nx + i, g.nx + 1, g.nx};
-    f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+    f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_of(f.ctl, dt_override), i, lj, a);
 }
 
-// ---------------------------------------------------------- v predictor (K2)
-
-// v* on global rows 1..=ny-1, columns 1..=nx-1 (model.rs:586-670 +
-// compute_vstar :439-521).  Advecting u is the raw face value U(i+1,j),
-// U(i,j).  SecondOrder: the lane of column nx-1 is never filled (:647-650),
-// so all six inputs are 0.0 there.
-template <int SCHEME, int SP, class A>
-__device__ __forceinline__ float v_pred_val(const Geom &g, const Fields &f, float dt_override,
-                                            int i, int lj, const A &a) {
-    const int nx = g.nx, ny = g.ny;
-    const int j = g.j0 + lj;
-    const long cv = (long)lj * nx + i;
-    const float vc = a.V(0, 0), ve1 = a.V(1, 0), vw1 = a.V(-1, 0), vn1 = a.V(0, 1), vs1 = a.V(0, -1);
-    float uE = a.U(1, 0), uW = a.U(0, 0);
-    float ve, vw, vn, vs;
-    if (SCHEME == 0) {
-        // v_face_{e,w,n,s}_first_order(_scalar) (:1073-1095, :1116-1142, :1163-1185, :1207-1229)
-        ve = (uE >= 0.0f) ? vc : ve1;
-        vw = (uW >= 0.0f) ? vw1 : vc;
-        vn = (0.5f * (vc + vn1) >= 0.0f) ? vc : vn1;
-        vs = (0.5f * (vs1 + vc) >= 0.0f) ? vs1 : vc;
-    } else if (i >= nx - 1) {
-        uE = 0.0f;
-        uW = 0.0f;
-        ve = vw = vn = vs = 0.0f;
-    } else {
-        const size_t vlen = (size_t)nx * (size_t)(ny + 1);
-        const size_t idx = (size_t)i + (size_t)j * nx;
-        // v_face_e_second_order (:1098-1113)
-        if (uE >= 0.0f) {
-            ve = (i > 0) ? 1.5f * vc - 0.5f * vw1 : vc;
-        } else if (idx + 2 < vlen && i < nx - 2) {
-            ve = 1.5f * ve1 - 0.5f * a.V(2, 0);
-        } else {
-            ve = ve1;
-        }
-        // v_face_w_second_order (:1145-1160)
-        if (uW >= 0.0f) {
-            vw = (i > 1) ? 1.5f * vw1 - 0.5f * a.V(-2, 0) : vw1;
-        } else {
-            vw = (i < nx - 1) ? 1.5f * vc - 0.5f * ve1 : vc;
-        }
-        // v_face_n_second_order (:1188-1204)
-        if (0.5f * (vc + vn1) >= 0.0f) {
-            vn = (j > 1) ? 1.5f * vc - 0.5f * vs1 : vc;
-        } else if ((size_t)i + (size_t)(j + 2) * nx < vlen && j < ny - 1) {
-            vn = 1.5f * vn1 - 0.5f * a.V(0, 2);
-        } else {
-            vn = vn1;
-        }
-        // v_face_s_second_order (:1232-1248)
-        if (0.5f * (vs1 + vc) >= 0.0f) {
-            vs = (j > 1) ? 1.5f * vs1 - 0.5f * a.V(0, -2) : vs1;
-        } else if (j < ny) {
-            vs = 1.5f * vc - 0.5f * vn1;
-        } else {
-            vs = vc;
-        }
-    }
-    float r;
-    if (f.any_pmask && (f.mask_v[cv] & 1)) {
-        r = 0.0f;
-    } else {
-        const float dx = g.dx, dy = g.dy, nu = g.nu;
-        const float dt = dt_of(f.ctl, dt_override);
-        const float f_e = uE * ve;
-        const float f_w = uW * vw;
-        const float f_n = vn * vn;
-        const float f_s = vs * vs;
-        const float convective = sdiv<SP>(f_e - f_w, dx, g.r_dx) + sdiv<SP>(f_n - f_s, dy, g.r_dy);
-        const float laplace = sdiv<SP>(ve1 - 2.0f * vc + vw1, dx * dx, g.r_dxx) +
-                              sdiv<SP>(vn1 - 2.0f * vc + vs1, dy * dy, g.r_dyy);
-        r = vc + dt * (-convective + nu * laplace);
-    }
-    return r;
-}
 
 template <int SCHEME, int SP>
 __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float dt_override,
@@ -254,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void k_v_predictor(Geom g, Fields f, float 
     const int lj = row_lo + bid / nbx;
     if (i > g.nx - 1) return;
     const GAcc a{f.u, f.v, (long)lj * (g.nx + 1) + i, (long)lj * g.nx + i, g.nx + 1, g.nx};
-    f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+    f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_of(f.ctl, dt_override), i, lj, a);
 }
 
 // Both predictors in one pass (piso_step's K1 + K2): each thread computes the
@@ -272,9 +120,9 @@ __global__ __launch_bounds__(kBlock) void k_predict(Geom g, Fields f, float dt_o
     const int lj = row_lo + bid / nbx;
     const GAcc a{f.u, f.v, (long)lj * (g.nx + 1) + i, (long)lj * g.nx + i, g.nx + 1, g.nx};
     if (lj <= u_hi && i <= g.nx)
-        f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+        f.u_star[(long)lj * (g.nx + 1) + i] = u_pred_val<SCHEME, SP>(g, f, dt_of(f.ctl, dt_override), i, lj, a);
     if (lj <= v_hi && i <= g.nx - 1)
-        f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_override, i, lj, a);
+        f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_of(f.ctl, dt_override), i, lj, a);
 }
 
 // Register-backed stencil for k_predict4: u rows lj-1..lj+1 and v rows
@@ -306,6 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_predict4(Geom g, Fields f, float dt_
     const int lj = row_lo + bid / nbx;
     const int nx = g.nx, W = nx + 1;
     if (i0 >= nx) return;
+    const float dtv = dt_of(f.ctl, dt_override);   // once: a per-face reload waits on every load
     const float *__restrict__ u = f.u;
     const float *__restrict__ v = f.v;
     const long ku = (long)lj * W + i0, kv = (long)lj * nx + i0;
@@ -342,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_predict4(Geom g, Fields f, float dt_
         float o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            o[q] = u_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAcc{ur, vr, q});
+            o[q] = u_pred_val<0, SP>(g, f, dtv, i0 + q, lj, RAcc{ur, vr, q});
         float *__restrict__ us = f.u_star + ku;
         if (i0 > 0) us[0] = o[0];
         us[1] = o[1];
@@ -350,14 +199,14 @@ __global__ __launch_bounds__(kBlock) void k_predict4(Geom g, Fields f, float dt_
         us[3] = o[3];
         if (i0 + 4 == nx) {
             const GAcc a{f.u, f.v, ku + 4, kv + 4, W, nx};
-            us[4] = u_pred_val<0, SP>(g, f, dt_override, nx, lj, a);
+            us[4] = u_pred_val<0, SP>(g, f, dtv, nx, lj, a);
         }
     }
     if (do_v) {
         float o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            o[q] = v_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAcc{ur, vr, q});
+            o[q] = v_pred_val<0, SP>(g, f, dtv, i0 + q, lj, RAcc{ur, vr, q});
         float *__restrict__ vs = f.v_star + kv;
         if (i0 > 0) {
             *reinterpret_cast<float4 *>(vs) = make_float4(o[0], o[1], o[2], o[3]);
@@ -391,6 +240,7 @@ __global__ __launch_bounds__(kBlock) void k_predict4r(Geom g, Fields f, float dt
     const int lj0 = row_lo + (bid / nbx) * RPT;
     const int nx = g.nx, W = nx + 1;
     if (i0 >= nx) return;
+    const float dtv = dt_of(f.ctl, dt_override);   // once: a per-face reload waits on every load
     const float *__restrict__ u = f.u;
     const float *__restrict__ v = f.v;
     const int u_cap = u_hi + 1 > v_hi ? u_hi + 1 : v_hi;   // last u row any face reads
@@ -418,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_predict4r(Geom g, Fields f, float dt
             float o[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                o[q] = u_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAccN{ur + r, vr + r, q});
+                o[q] = u_pred_val<0, SP>(g, f, dtv, i0 + q, lj, RAccN{ur + r, vr + r, q});
             float *__restrict__ us = f.u_star + ku;
             if (i0 > 0) us[0] = o[0];
             us[1] = o[1];
@@ -426,14 +276,14 @@ __global__ __launch_bounds__(kBlock) void k_predict4r(Geom g, Fields f, float dt
             us[3] = o[3];
             if (i0 + 4 == nx) {
                 const GAcc a{f.u, f.v, ku + 4, kv + 4, W, nx};
-                us[4] = u_pred_val<0, SP>(g, f, dt_override, nx, lj, a);
+                us[4] = u_pred_val<0, SP>(g, f, dtv, nx, lj, a);
             }
         }
         if (lj <= v_hi) {
             float o[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                o[q] = v_pred_val<0, SP>(g, f, dt_override, i0 + q, lj, RAccN{ur + r, vr + r, q});
+                o[q] = v_pred_val<0, SP>(g, f, dtv, i0 + q, lj, RAccN{ur + r, vr + r, q});
             float *__restrict__ vs = f.v_star + kv;
             if (i0 > 0) {
                 *reinterpret_cast<float4 *>(vs) = make_float4(o[0], o[1], o[2], o[3]);
@@ -552,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void k_predict_div(Geom g, Fields f, float 
         if (rr >= glo && rr <= v_hi) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                vs[k][q] = v_pred_val<0, SP>(g, f, dt_override, i0 + q, rr,
+                vs[k][q] = v_pred_val<0, SP>(g, f, dt, i0 + q, rr,
                                              RAcc3{ur[k + 1], ur[k + 1], ur[k + 1], vr[k], vr[k + 1],
                                                    vr[k + 2], q});
             if (i0 == 0) vs[k][0] = f.v_star[(long)rr * nx];   // column 0 is not predicted
@@ -582,7 +432,7 @@ __global__ __launch_bounds__(kBlock) void k_predict_div(Geom g, Fields f, float 
         if (upred) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                us[q] = u_pred_val<0, SP>(g, f, dt_override, i0 + q, r,
+                us[q] = u_pred_val<0, SP>(g, f, dt, i0 + q, r,
                                           RAcc3{ur[k], ur[k + 1], ur[k + 2], vr[k], vr[k + 1],
                                                 vr[k + 2], q});
             if (i0 == 0) us[0] = f.u_star[ku];   // face 0 is not predicted
@@ -594,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void k_predict_div(Geom g, Fields f, float 
         if (i0 + 4 == nx) {
             if (upred) {
                 const GAcc a{f.u, f.v, ku + 4, (long)r * nx + i0 + 4, W, nx};
-                east = u_pred_val<0, SP>(g, f, dt_override, nx, r, a);
+                east = u_pred_val<0, SP>(g, f, dt, nx, r, a);
             } else {
                 east = f.u_star[ku + 4];
             }
@@ -1347,7 +1197,7 @@ void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream
 
 bool predict_div_fused(const Geom &g, const Fields &f) {
     auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-    return g.pred_div && g.scheme == 0 && g.nx % 4 == 0 && g.nx >= 8 && a16(f.v) && a16(f.v_star) &&
+    return g.pred_div == 1 && g.scheme == 0 && g.nx % 4 == 0 && g.nx >= 8 && a16(f.v) && a16(f.v_star) &&
            a16(f.rhs);
 }
 

@@ -644,8 +644,11 @@ struct cfd_model {
     // the boundaries and the step reductions run as one fused pass.
     int enqueue_piso(float dt_override, bool finish = false) {
         // K1-K3: the fused march when it applies, else predictors + divergence
-        const bool fused = predict_div_fused(g, f);
-        if (fused)
+        const bool march = predict_march_ok(g, f);
+        const bool fused = march || predict_div_fused(g, f);
+        if (march)
+            launch_predict_march(g, f, dt_override, stream);
+        else if (fused)
             launch_predict_div(g, f, dt_override, stream);
         else
             launch_predict(g, f, dt_override, stream);
@@ -914,8 +917,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // division the march is VALU-bound and kind 4 at T = 4 stays (r1: 6144^2
     // 7.3e11 vs 6.1e11 cell-updates/s at T = 8).  Single domain and slabs alike.
     g.tb_kind = g.fastdiv == 1 ? 5 : 4;
-    g.pred_div = 1;
-    if (const char *e = getenv("CFD_PRED_DIV")) g.pred_div = atoi(e) != 0;
+    g.pred_div = 2;
+    if (const char *e = getenv("CFD_PRED_DIV")) g.pred_div = std::min(std::max(atoi(e), 0), 2);
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
         g.tb_kind = (k == 3 || k == 4 || k == 5) ? k : 1;

@@ -153,14 +153,17 @@ def test_fused_finish_channel(scheme, profile, tol):
         assert_bitwise(f, st[f], o.field(f))
 
 
-@pytest.mark.parametrize("case", ["cavity", "channel_fo", "channel_passes", "wide_ragged"])
+@pytest.mark.parametrize("case", ["cavity", "channel_fo", "channel_passes", "wide_ragged",
+                                  "cavity_so", "channel_so", "wide_ragged_so", "tall_so"])
 def test_predict_div_fused_matches_unfused(monkeypatch, case):
-    """k_predict_div (first-order predictors + divergence in one row march) vs
-    the separate k_predict4r + k_divergence launches, every field bitwise:
-    segment edges (ny not a multiple of the 16-row segment), wave columns of
-    63 chunks (nx/4 not a multiple of 63), face 0 / face nx / column 0 read
-    from memory, obstacle masks, corrector passes (later divergences unfused)."""
+    """The fused predictor + divergence kernels vs the separate predictor and
+    k_divergence launches, every field bitwise: k_predict_march (CFD_PRED_DIV=2,
+    both schemes) and k_predict_div (=1, first order).  Covers segment edges
+    (ny not a multiple of the segment), wave columns of 62 / 63 chunks (nx/4 + 1
+    not a multiple), face 0 / face nx / column 0, the flat wrap reads of the
+    last chunk, obstacle masks, corrector passes (later divergences unfused)."""
     c = _cfd()
+    so = c.VelocityScheme.SecondOrder
     cases = {
         "cavity": (c.cavity_grid(64, 48), c.SimulationParams.cavity(100.0, 30, tol_enabled=False), 6),
         "channel_fo": (c.Grid(256, 200, 30.0, 10.0, c.Cylinder(7.5, 5.0, 0.75)),
@@ -168,18 +171,28 @@ def test_predict_div_fused_matches_unfused(monkeypatch, case):
         "channel_passes": (c.Grid(192, 96, 30.0, 10.0, c.Cylinder(7.5, 5.0, 1.5)),
                            c.SimulationParams(corrector_passes=3, jacobi_iters=20), 4),
         "wide_ragged": (c.cavity_grid(1016, 37), c.SimulationParams.cavity(400.0, 12, tol_enabled=False), 3),
+        "cavity_so": (c.cavity_grid(64, 48), c.SimulationParams.cavity(100.0, 30, tol_enabled=False,
+                                                                      velocity_scheme=so), 8),
+        "channel_so": (c.Grid(256, 200, 30.0, 10.0, c.Cylinder(7.5, 5.0, 0.75)),
+                       c.SimulationParams(corrector_passes=2, velocity_scheme=so), 6),
+        "wide_ragged_so": (c.cavity_grid(1016, 37), c.SimulationParams.cavity(
+            400.0, 12, tol_enabled=False, velocity_scheme=so), 4),
+        "tall_so": (c.Grid(248, 301, 8.0, 10.0, c.Cylinder(4.0, 5.0, 1.0)),
+                    c.SimulationParams(corrector_passes=0, jacobi_iters=15, velocity_scheme=so), 5),
     }
     grid, params, steps = cases[case]
+    modes = ("0", "2") if params.velocity_scheme == so else ("0", "1", "2")
     out = {}
-    for fused in ("0", "1"):
+    for fused in modes:
         monkeypatch.setenv("CFD_PRED_DIV", fused)
         m = c.Model(grid, params)
         for _ in range(steps):
             m.update()
         out[fused] = m.get_state()
         m.close()
-    for f in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
-        assert_bitwise(f, out["1"][f], out["0"][f])
+    for mode in modes[1:]:
+        for f in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
+            assert_bitwise(f"{f} (CFD_PRED_DIV={mode})", out[mode][f], out["0"][f])
 
 
 def test_jacobi_tolerance_and_fixed_paths():
