@@ -122,6 +122,12 @@ struct cfd_model {
     ncclComm_t comm = nullptr;
     LocalHub *hub = nullptr;   // testing stand-in for comm
     int host_cur = 0;   // mirror of ctl->cur, valid when the tolerance is off
+    // SOR: one fused launch per red-black iteration (k_sor_fused) where it
+    // applies; CFD_SOR_FUSED=0 keeps the two color passes in place
+    bool sor_fused = [] {
+        const char *e = getenv("CFD_SOR_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
     // p' ghost rows deeper than 1 are stale (a host-driven tolerance solve or
     // cfd_profile_sweeps refreshed only one row per sweep): the next deep-halo
     // fixed-count solve re-exchanges hg rows before its first sweep
@@ -343,6 +349,19 @@ struct cfd_model {
         k.r_dx2 = r[0];
         k.r_dy2 = r[1];
         k.r_denom = r[2];
+        if (iters > 0 && sor_fused && sor_fused_ok(g.nx, g.ny)) {
+            // one launch per iteration, ping-pong from the device's current
+            // buffer; the finalize flips it once per executed iteration
+            for (int it = 0; it < iters; ++it)
+                launch_sor_fused(f.pp[0], f.pp[1], f.rhs, g.nx, g.ny, k, f.ctl, f.err_slots, pass,
+                                 it, g.tol_enabled, g.p_tol, g.tol_enabled || it == iters - 1,
+                                 stream);
+            end_solve_timing(e0, (uint64_t)iters, (uint64_t)iters);
+            launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, iters, stream);
+            if (!g.tol_enabled) host_cur = (host_cur + iters) & 1;
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
         float *pp = f.pp[host_cur];
         launch_fill_zero(pp, (size_t)g.nx * g.ny, f.ctl, pass, stream);
         for (int it = 0; it < iters; ++it) {

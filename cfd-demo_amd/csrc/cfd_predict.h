@@ -26,7 +26,9 @@ struct GAcc {
 // u* on global rows 1..=ny-2, faces 1..=nx (model.rs:538-580 + compute_ustar
 // :382-436).  One thread per face; neighbour reuse comes from L1/L2.  Flux
 // velocities are the raw v values (get_v_north/south :1056-1069).
-template <int SCHEME, int SP, class A>
+// INT: the caller guarantees an interior face (3 <= i <= nx-2, 2 <= j <=
+// ny-3), where every column / row test of the second-order faces holds.
+template <int SCHEME, int SP, bool INT = false, class A>
 __device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, float dt,
                                             int i, int lj, const A &a) {
     const int nx = g.nx, ny = g.ny, W = nx + 1;
@@ -41,39 +43,32 @@ __device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, floa
         un = (vn >= 0.0f) ? uc : un1;
         us = (vs >= 0.0f) ? us1 : uc;
     } else {
-        const size_t ulen = (size_t)W * (size_t)ny;
+        // The reference's bounds checks on flat indices reduce, over the faces
+        // it predicts (1 <= i <= nx, 1 <= j <= ny-2, pitch W = nx+1, length
+        // W*ny), to plain row / column tests:
+        //   (i+1) + j*W + 1 < W*ny  <=>  i+2 < W*(ny-j), true as ny-j >= 2;
+        //   i + (j+2)*W < W*ny      <=>  i < W*(ny-j-2)  <=>  j < ny-2.
+        // Every candidate is formed and the upwind decision selects one
+        // (same values as the reference's if / else chains; selects instead
+        // of divergent branches).
         // u_face_e_second_order (:911-926)
-        if (uc >= 0.0f) {
-            ue = (i > 1) ? 1.5f * uc - 0.5f * a.U(-1, 0) : uc;
-        } else if (((size_t)(i + 1) + (size_t)j * W) + 1 < ulen && i < nx - 1) {
-            ue = 1.5f * ue1 - 0.5f * a.U(2, 0);
-        } else {
-            ue = ue1;
-        }
+        const float ue_p = (INT || i > 1) ? 1.5f * uc - 0.5f * a.U(-1, 0) : uc;
+        const float ue_m = (INT || i < nx - 1) ? 1.5f * ue1 - 0.5f * a.U(2, 0) : ue1;
+        ue = (uc >= 0.0f) ? ue_p : ue_m;
         // u_face_w_second_order (:944-963)
-        if (uw1 >= 0.0f) {
-            uw = (i > 2) ? 1.5f * uw1 - 0.5f * a.U(-2, 0) : uw1;
-        } else {
-            uw = (i < nx) ? 1.5f * uc - 0.5f * ue1 : uc;
-        }
+        const float uw_p = (INT || i > 2) ? 1.5f * uw1 - 0.5f * a.U(-2, 0) : uw1;
+        const float uw_m = (INT || i < nx) ? 1.5f * uc - 0.5f * ue1 : uc;
+        uw = (uw1 >= 0.0f) ? uw_p : uw_m;
         // u_face_n_second_order (:992-1008), decision on averaged v (:983-989)
         const float vnb = 0.5f * (a.V(-1, 1) + a.V(0, 1));
-        if (vnb >= 0.0f) {
-            un = (j > 1) ? 1.5f * uc - 0.5f * us1 : uc;
-        } else if ((size_t)i + (size_t)(j + 2) * W < ulen && j < ny - 1) {
-            un = 1.5f * un1 - 0.5f * a.U(0, 2);
-        } else {
-            un = un1;
-        }
+        const float un_p = (INT || j > 1) ? 1.5f * uc - 0.5f * us1 : uc;
+        const float un_m = (INT || j < ny - 2) ? 1.5f * un1 - 0.5f * a.U(0, 2) : un1;
+        un = (vnb >= 0.0f) ? un_p : un_m;
         // u_face_s_second_order (:1037-1053), decision on averaged v (:1028-1034)
         const float vsb = 0.5f * (a.V(-1, 0) + a.V(0, 0));
-        if (vsb >= 0.0f) {
-            us = (j > 1) ? 1.5f * us1 - 0.5f * a.U(0, -2) : us1;
-        } else if (j < ny) {
-            us = 1.5f * uc - 0.5f * un1;
-        } else {
-            us = uc;
-        }
+        const float us_p = (INT || j > 1) ? 1.5f * us1 - 0.5f * a.U(0, -2) : us1;
+        const float us_m = (INT || j < ny) ? 1.5f * uc - 0.5f * un1 : uc;
+        us = (vsb >= 0.0f) ? us_p : us_m;
     }
     const float dx = g.dx, dy = g.dy, nu = g.nu;
     const float f_e = ue * ue;
@@ -94,7 +89,9 @@ __device__ __forceinline__ float u_pred_val(const Geom &g, const Fields &f, floa
 // compute_vstar :439-521).  Advecting u is the raw face value U(i+1,j),
 // U(i,j).  SecondOrder: the lane of column nx-1 is never filled (:647-650),
 // so all six inputs are 0.0 there.
-template <int SCHEME, int SP, class A>
+// INT: interior face (2 <= i <= nx-3, 2 <= j <= ny-2): every column / row test
+// of the second-order faces holds.
+template <int SCHEME, int SP, bool INT = false, class A>
 __device__ __forceinline__ float v_pred_val(const Geom &g, const Fields &f, float dt,
                                             int i, int lj, const A &a) {
     const int nx = g.nx, ny = g.ny;
@@ -109,50 +106,38 @@ __device__ __forceinline__ float v_pred_val(const Geom &g, const Fields &f, floa
         vw = (uW >= 0.0f) ? vw1 : vc;
         vn = (0.5f * (vc + vn1) >= 0.0f) ? vc : vn1;
         vs = (0.5f * (vs1 + vc) >= 0.0f) ? vs1 : vc;
-    } else if (i >= nx - 1) {
+    } else if (!INT && i >= nx - 1) {
         uE = 0.0f;
         uW = 0.0f;
         ve = vw = vn = vs = 0.0f;
     } else {
-        const size_t vlen = (size_t)nx * (size_t)(ny + 1);
-        const size_t idx = (size_t)i + (size_t)j * nx;
+        // Bounds checks on flat indices over the faces predicted here
+        // (1 <= i <= nx-2, 1 <= j <= ny-1, length nx*(ny+1)):
+        //   i + j*nx + 2 < nx*(ny+1)      <=>  i+2 < nx*(ny+1-j), true;
+        //   i + (j+2)*nx < nx*(ny+1)      <=>  j <= ny-2.
         // v_face_e_second_order (:1098-1113)
-        if (uE >= 0.0f) {
-            ve = (i > 0) ? 1.5f * vc - 0.5f * vw1 : vc;
-        } else if (idx + 2 < vlen && i < nx - 2) {
-            ve = 1.5f * ve1 - 0.5f * a.V(2, 0);
-        } else {
-            ve = ve1;
-        }
+        const float ve_p = (INT || i > 0) ? 1.5f * vc - 0.5f * vw1 : vc;
+        const float ve_m = (INT || i < nx - 2) ? 1.5f * ve1 - 0.5f * a.V(2, 0) : ve1;
+        ve = (uE >= 0.0f) ? ve_p : ve_m;
         // v_face_w_second_order (:1145-1160)
-        if (uW >= 0.0f) {
-            vw = (i > 1) ? 1.5f * vw1 - 0.5f * a.V(-2, 0) : vw1;
-        } else {
-            vw = (i < nx - 1) ? 1.5f * vc - 0.5f * ve1 : vc;
-        }
+        const float vw_p = (INT || i > 1) ? 1.5f * vw1 - 0.5f * a.V(-2, 0) : vw1;
+        const float vw_m = (INT || i < nx - 1) ? 1.5f * vc - 0.5f * ve1 : vc;
+        vw = (uW >= 0.0f) ? vw_p : vw_m;
         // v_face_n_second_order (:1188-1204)
-        if (0.5f * (vc + vn1) >= 0.0f) {
-            vn = (j > 1) ? 1.5f * vc - 0.5f * vs1 : vc;
-        } else if ((size_t)i + (size_t)(j + 2) * nx < vlen && j < ny - 1) {
-            vn = 1.5f * vn1 - 0.5f * a.V(0, 2);
-        } else {
-            vn = vn1;
-        }
+        const float vn_p = (INT || j > 1) ? 1.5f * vc - 0.5f * vs1 : vc;
+        const float vn_m = (INT || j < ny - 1) ? 1.5f * vn1 - 0.5f * a.V(0, 2) : vn1;
+        vn = (0.5f * (vc + vn1) >= 0.0f) ? vn_p : vn_m;
         // v_face_s_second_order (:1232-1248)
-        if (0.5f * (vs1 + vc) >= 0.0f) {
-            vs = (j > 1) ? 1.5f * vs1 - 0.5f * a.V(0, -2) : vs1;
-        } else if (j < ny) {
-            vs = 1.5f * vc - 0.5f * vn1;
-        } else {
-            vs = vc;
-        }
+        const float vs_p = (INT || j > 1) ? 1.5f * vs1 - 0.5f * a.V(0, -2) : vs1;
+        const float vs_m = (INT || j < ny) ? 1.5f * vc - 0.5f * vn1 : vc;
+        vs = (0.5f * (vs1 + vc) >= 0.0f) ? vs_p : vs_m;
     }
     float r;
     if (f.any_pmask && (f.mask_v[cv] & 1)) {
         r = 0.0f;
     } else {
         const float dx = g.dx, dy = g.dy, nu = g.nu;
-            const float f_e = uE * ve;
+        const float f_e = uE * ve;
         const float f_w = uW * vw;
         const float f_n = vn * vn;
         const float f_s = vs * vs;

@@ -35,8 +35,11 @@
 namespace cfd {
 namespace {
 
+#ifndef CFD_PM_WPE
+#define CFD_PM_WPE 3  // minimum waves per SIMD (caps VGPRs at 168)
+#endif
 #ifndef CFD_PM_PD
-#define CFD_PM_PD 2   // prefetch distance (steps) of the u / v rows
+#define CFD_PM_PD 1   // prefetch distance (steps) of the u / v rows (1: 88.6 vs 90.3 us SO, r2 pm)
 #endif
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -102,8 +105,11 @@ struct PredMarch {
     // reference does not predict, read from memory, and the segment end).
     // The steady state (GEN false) has no load under a branch, so the
     // compiler's wait counts never drain the rows in flight.
-    template <int T_, bool GEN>
+    // INT: the wave's columns and the steady steps' rows are interior
+    // (u_pred_val / v_pred_val skip their column and row tests)
+    template <int T_, bool GEN, bool INT>
     __device__ __forceinline__ void step(int t) {
+        constexpr bool I = INT && !GEN;
         const int k = kb + t;
         const int nx = g->nx;
         Fields ff = f;
@@ -144,7 +150,7 @@ struct PredMarch {
         if (!GEN || (rv >= glo && rv <= v_hi)) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                vn[q] = v_pred_val<SCHEME, SP>(*g, ff, dt, min(i0 + q, nx - 1), rv,
+                vn[q] = v_pred_val<SCHEME, SP, I>(*g, ff, dt, min(i0 + q, nx - 1), rv,
                                                MAcc<3>{ux, vx, q});
             if (c == 0) vn[0] = vb;   // column 0 is not predicted
             if (st_lane && c < nch && (!GEN || t > 0 || r0 == 0))
@@ -163,7 +169,7 @@ struct PredMarch {
             if (upred) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    us[q] = u_pred_val<SCHEME, SP>(*g, ff, dt, min(i0 + q, nx), k, MAcc<2>{ux, vx, q});
+                    us[q] = u_pred_val<SCHEME, SP, I>(*g, ff, dt, min(i0 + q, nx), k, MAcc<2>{ux, vx, q});
                 if (c == 0) us[0] = ub;   // face 0 is not predicted
             } else if (c <= nch) {
                 const f4u a = *reinterpret_cast<const f4u *>(f.u_star + ku);
@@ -203,22 +209,23 @@ struct PredMarch {
     // the segment's R + 1 steps, fully unrolled (every ring index and step
     // kind compile-time, no loop back edge whose register copies would wait
     // for the rows in flight): t = 0, 1 and R general, the rest steady
-    template <int T>
+    template <int T, bool INT>
     __device__ __forceinline__ void steps() {
         if constexpr (T <= R) {
-            step<T % D, (T < 2 || T == R)>(T);
-            steps<T + 1>();
+            step<T % D, (T < 2 || T == R), INT>(T);
+            steps<T + 1, INT>();
         }
     }
+    template <bool INT>
     __device__ __forceinline__ void run() {
 #pragma unroll
         for (int t = 0; t < D; ++t) ld_rows(t, t);
-        steps<0>();
+        steps<0, INT>();
     }
 };
 
 template <int SCHEME, int SP, bool MASK, int R>
-__global__ __launch_bounds__(kBlock) void k_predict_march(Geom g, Fields f, float dt_override,
+__global__ __launch_bounds__(kBlock, CFD_PM_WPE) void k_predict_march(Geom g, Fields f, float dt_override,
                                                           int glo, int u_hi, int v_hi, int nwc,
                                                           int nseg) {
     PredMarch<SCHEME, SP, MASK, R> m;
@@ -254,7 +261,17 @@ __global__ __launch_bounds__(kBlock) void k_predict_march(Geom g, Fields f, floa
     m.dt = dt_of(f.ctl, dt_override);
 #pragma unroll
     for (int q = 0; q < 4; ++q) m.vs[q] = 0.0f;
-    m.run();
+    // interior wave: every chunk it touches has columns in [3, nx-3] (so the
+    // last chunk nch is not among them), and the steady steps' faces (u row
+    // k, v row k+1, k = r0+1 .. r1-2) lie on global rows [2, ny-3] / [2, ny-2]
+    const int c_lo = wc * 62 - 1, c_hi = wc * 62 + 62;
+    const bool interior = 4 * c_lo >= 3 && 4 * c_hi + 3 <= nx - 3 &&
+                          g.j0 + m.r0 + 1 >= 2 && g.j0 + m.r1 - 2 <= g.ny - 3;
+    // the interior form only where it changes the code (second order)
+    if (SCHEME == 1 && interior)
+        m.template run<true>();
+    else
+        m.template run<false>();
 }
 
 }  // namespace
@@ -270,13 +287,11 @@ void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hip
     const int glo = (g.j0 > 1 ? g.j0 : 1) - g.j0;
     const int u_hi = ((g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2)) - g.j0;
     const int v_hi = ((g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1)) - g.j0;
-    // rows per segment: 16 (one round of ~4 waves per SIMD at 4096^2 with 17
-    // wave columns; CFD_PM_ROWS=8 selects 8), 4 on slabs under 16 rows
-    static const int rows_env = [] {
-        const char *e = getenv("CFD_PM_ROWS");
-        return e && atoi(e) == 8 ? 8 : 16;
-    }();
-    const int rows = g.nyl >= rows_env ? rows_env : 4;
+    // rows per segment: 8 (two rounds of ~3-4 waves per SIMD at 4096^2 with
+    // 17 wave columns; 16-row segments measured equal for the first-order
+    // scheme and 17 % slower for the second-order one, whose unrolled march
+    // then outgrows the instruction cache), 4 on slabs under 8 rows
+    const int rows = g.nyl >= 8 ? 8 : 4;
     const int nwc = cdiv(g.nx / 4 + 1, 62);
     const int nseg = cdiv(g.nyl, rows);
     const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
@@ -284,7 +299,7 @@ void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hip
     hipLaunchKernelGGL((k_predict_march<SC, SPV, MK, R>), grid, dim3(kBlock), 0, s, g, f, dt_override, \
                        glo, u_hi, v_hi, nwc, nseg)
 #define CFD_LAUNCH_PM3(SC, SPV, MK) \
-    if (rows == 16) CFD_LAUNCH_PM(SC, SPV, MK, 16); else if (rows == 8) CFD_LAUNCH_PM(SC, SPV, MK, 8); else CFD_LAUNCH_PM(SC, SPV, MK, 4)
+    if (rows == 8) CFD_LAUNCH_PM(SC, SPV, MK, 8); else CFD_LAUNCH_PM(SC, SPV, MK, 4)
 #define CFD_LAUNCH_PM2(SC, SPV) \
     if (f.any_pmask) { CFD_LAUNCH_PM3(SC, SPV, true); } else { CFD_LAUNCH_PM3(SC, SPV, false); }
     if (g.scheme == 0) {

@@ -92,6 +92,126 @@ __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
                     bid * (kBlock / 64) + ((int)threadIdx.x >> 6), m);
 }
 
+// One whole red-black SOR iteration in one launch (both colors), p' read from
+// `src` and written to the other buffer, so p' and rhs cross HBM once per
+// iteration (12 B per cell-update) instead of once per color.  A wave owns 64
+// lanes x one column pair (one red and one black cell per row) and a segment
+// of R interior rows [r0, r0+R); all rows it needs — p' rows r0-2..r0+R+1 and
+// rhs rows r0-1..r0+R — are loaded up front, then
+//   red  rows r0-1..r0+R   from the old black neighbours (src),
+//   black rows r0..r0+R-1  from the new red ones (registers),
+// exactly the two color passes of k_sor_color over the same values: a red
+// update reads only old black cells and boundary cells, a black update only
+// new red cells (its vertical and horizontal neighbours have the other
+// parity) and boundary cells, which no pass of the iteration changes.  The
+// boundary conditions are stored as k_sor_color's black pass stores them.
+// Horizontal neighbours come from the adjacent lanes (DPP); lanes 0 and 63
+// only feed them, so waves step 62 pairs.  Iteration 0 reads no source: the
+// solve starts from p' = 0 (index.html:743).  The last segment of a column
+// ends at row ny-1 and overlaps its neighbour (identical stores).
+template <int FAST, int R>
+__global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ pa,
+                                                      const float *__restrict__ pb,
+                                                      float *__restrict__ qa, float *__restrict__ qb,
+                                                      const float *__restrict__ rhs, int nx, int ny,
+                                                      SorConst k, Ctl *ctl, uint32_t *err_slots,
+                                                      int pass, int it, int tol, float p_tol,
+                                                      int res, int nwc, int nseg) {
+    if (pass_off(ctl, pass)) return;
+    if (tol && it > 0 &&
+        read_max(err_slots + (size_t)(it - 1) * kResSlots * kResStride, ctl->err[it - 1]) < p_tol)
+        return;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int lane = (int)threadIdx.x & 63;
+    const int bid = (int)blockIdx.x;
+    const int wc = bid % nwc;
+    const int seg = (bid / nwc) * (kBlock / 64) + wave;
+    if (seg >= nseg) return;   // wave-uniform
+    // buffers alternate per iteration from the solve's current one
+    const int si = (ctl->cur + it) & 1;
+    const float *__restrict__ src = si ? pb : pa;
+    float *__restrict__ dst = si ? qa : qb;
+    const int r0 = 1 + min(seg * R, ny - 2 - R);
+    const int c = wc * 62 - 1 + lane;
+    const bool in_dom = c >= 0 && 2 * c < nx;
+    const bool out = in_dom && lane >= 1 && lane <= 62;
+    const int i0 = 2 * c;
+    float2 A[R + 4], Rh[R + 2];   // p' rows r0-2+q, rhs rows r0-1+q
+#pragma unroll
+    for (int q = 0; q < R + 4; ++q) {
+        const int r = min(max(r0 - 2 + q, 0), ny - 1);
+        A[q] = (in_dom && it > 0) ? *reinterpret_cast<const float2 *>(src + (long)r * nx + i0)
+                                  : make_float2(0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int q = 0; q < R + 2; ++q) {
+        const int r = min(max(r0 - 1 + q, 0), ny - 1);
+        Rh[q] = in_dom ? *reinterpret_cast<const float2 *>(rhs + (long)r * nx + i0)
+                       : make_float2(0.0f, 0.0f);
+    }
+    const double omega = 1.7;
+    float m = 0.0f;
+    // one cell: the script's update (index.html:749-760) in double, stored as f32
+    auto relax = [&](float p_old_f, float pe, float pw, float pn, float ps, float rh, bool upd,
+                     bool count) {
+        if (!upd) return p_old_f;
+        const double p_old = (double)p_old_f;
+        const double h = ddiv<FAST>((double)pe + (double)pw, k.dx2, k.r_dx2);
+        const double v = ddiv<FAST>((double)pn + (double)ps, k.dy2, k.r_dy2);
+        const double p_update = ddiv<FAST>(h + v - (double)rh, k.denom, k.r_denom);
+        const float nv = (float)((1.0 - omega) * p_old + omega * p_update);
+        if (count) m = fmaxf(m, (float)fabs((double)nv - p_old));
+        return nv;
+    };
+    // red cells of rows r0-1+q (q = 0..R+1): column i0 + (row & 1)
+    float red[R + 2];
+#pragma unroll
+    for (int q = 0; q < R + 2; ++q) {
+        const int r = r0 - 1 + q;   // wave-uniform
+        const float2 a = A[q + 1], up = A[q + 2], dn = A[q];
+        const bool row_in = r >= 1 && r <= ny - 2;
+        const bool count = out && q >= 1 && q <= R;
+        if ((r & 1) == 0) {   // red at x (column i0)
+            const int i = i0;
+            red[q] = relax(a.x, a.y, from_left(a.y), up.x, dn.x, Rh[q].x,
+                           row_in && i >= 1 && i <= nx - 2, count);
+        } else {              // red at y (column i0 + 1)
+            const int i = i0 + 1;
+            red[q] = relax(a.y, from_right(a.x), a.x, up.y, dn.y, Rh[q].y,
+                           row_in && i >= 1 && i <= nx - 2, count);
+        }
+    }
+    // black cells of rows r0+q (q = 0..R-1), the pair's final values, BCs
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int r = r0 + q;
+        const float2 a = A[q + 2];
+        const float rd = red[q + 1];
+        float2 o;
+        if ((r & 1) == 0) {   // red at x, black at y (column i0 + 1)
+            const int i = i0 + 1;
+            o.x = rd;
+            o.y = relax(a.y, from_right(rd), rd, red[q + 2], red[q], Rh[q + 1].y,
+                        i >= 1 && i <= nx - 2, out);
+        } else {              // black at x (column i0), red at y
+            const int i = i0;
+            o.y = rd;
+            o.x = relax(a.x, rd, from_left(rd), red[q + 2], red[q], Rh[q + 1].x,
+                        i >= 1 && i <= nx - 2, out);
+        }
+        if (i0 == 0) o.x = o.y;            // P(0,j) = P(1,j)
+        if (i0 + 1 == nx - 1) o.y = 0.0f;  // P(nx-1,j) = 0
+        if (out) {
+            *reinterpret_cast<float2 *>(dst + (long)r * nx + i0) = o;
+            if (r == 1) *reinterpret_cast<float2 *>(dst + i0) = o;                              // row 0
+            if (r == ny - 2) *reinterpret_cast<float2 *>(dst + (long)(ny - 1) * nx + i0) = o;  // row ny-1
+        }
+    }
+    if (!res) return;
+    m = wave_max(out ? m : 0.0f);
+    if (lane == 0) publish_max(err_slots + (size_t)it * kResSlots * kResStride, bid * (kBlock / 64) + wave, m);
+}
+
 // p' = 0 at the start of a solve (index.html:743, :777), gated by the
 // corrector loop like every solve kernel.
 __global__ __launch_bounds__(kBlock) void k_fill_zero(float4 *p, long n4, const Ctl *ctl, int pass) {
@@ -381,6 +501,8 @@ __global__ __launch_bounds__(kBlock) void k_mg_final_residual(MgLevel L, const f
     }
 }
 
+constexpr int kSorRows = 16;   // interior rows per k_sor_fused segment
+
 inline int grid_of(int nx, int ny, int *nbx) {
     *nbx = cdiv(nx, kBlock);
     return *nbx * ny;
@@ -401,6 +523,22 @@ void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorCons
     else
         hipLaunchKernelGGL(k_sor_color<0>, dim3(nbx * (ny - 2)), dim3(kBlock), 0, s, pp, rhs, nx, ny,
                            k, color, ctl, err_slots, pass, it, tol, p_tol, res, nbx);
+}
+
+bool sor_fused_ok(int nx, int ny) { return nx % 2 == 0 && nx >= 4 && ny - 2 >= kSorRows; }
+
+void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, const SorConst &k,
+                      Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
+                      hipStream_t s) {
+    const int nwc = cdiv(nx / 2, 62);
+    const int nseg = cdiv(ny - 2, kSorRows);
+    const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
+    if (k.fast)
+        hipLaunchKernelGGL((k_sor_fused<1, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs, nx,
+                           ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg);
+    else
+        hipLaunchKernelGGL((k_sor_fused<0, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs, nx,
+                           ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg);
 }
 
 void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s) {

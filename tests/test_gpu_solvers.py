@@ -58,13 +58,20 @@ def test_multigrid_solve_matches_reference_javascript(monkeypatch, name, tail, t
     assert st["jacobi_sweeps_total"] == 1
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("nx,ny,lx,ly,iters,tol,scale", [
     (64, 48, 4.0 / 3.0, 1.0, 40, False, 1.0),     # IEEE double division
     (128, 128, 1.0, 1.0, 60, False, 1.0),         # power-of-two divisors: reciprocal multiply
     (96, 72, 30.0, 10.0, 500, True, 1e-2),        # converges and exits early
-    (16, 4, 1.0, 1.0, 5, False, 1.0),             # smallest grid
+    (264, 150, 2.64, 1.5, 33, False, 1.0),        # 3 wave columns, ragged last segment
+    (256, 19, 1.0, 1.0, 7, True, 1.0),            # one 16-row segment, tolerance on
+    (16, 4, 1.0, 1.0, 5, False, 1.0),             # smallest grid (two color passes)
 ])
-def test_sor_solve_matches_oracle(nx, ny, lx, ly, iters, tol, scale):
+def test_sor_solve_matches_oracle(monkeypatch, fused, nx, ny, lx, ly, iters, tol, scale):
+    """k_sor_fused (one launch per red-black iteration, ping-pong buffers;
+    CFD_SOR_FUSED=1, the default where it applies) and the in-place two color
+    passes (=0) against the oracle's red-black restatement, bitwise."""
+    monkeypatch.setenv("CFD_SOR_FUSED", fused)
     c = _cfd()
     import oracle
     rng = np.random.default_rng(nx + ny)

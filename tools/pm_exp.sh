@@ -24,8 +24,15 @@ for p in glob.glob(f"gpurun_out/pm_{tag}/**/*kernel_stats.csv", recursive=True):
             print(f"{tag:>14} {nm:>44} calls {r['Calls']:>5} avg {float(r['AverageNs'])/1e3:8.2f} us")
 EOF
 }
-for v in 1 2; do CFD_PRED_DIV=$v TB_WARMUP=200 trace fo_pd$v tools/tb_one.py 4096 5; done
-for R in 8; do CFD_PM_ROWS=$R CFD_PRED_DIV=2 TB_WARMUP=200 trace fo_rows$R tools/tb_one.py 4096 5; done
-for v in 0 2; do CFD_PRED_DIV=$v trace so_pd$v tools/so_step.py; done
-CFD_PM_ROWS=8 CFD_PRED_DIV=2 trace so_rows8 tools/so_step.py
+for V in ${VARIANTS:-default}; do
+  if [ "$V" = default ]; then L=""; else L=cfd-demo_amd/lib/variants/$V/libcfd_amd.so; fi
+  CFD_LIB=$L TB_WARMUP=200 trace fo_$V tools/tb_one.py 4096 5
+  CFD_LIB=$L trace so_$V tools/so_step.py
+done
+if [ "${SOLVERS:-0}" = 1 ]; then
+  for v in 0 1; do
+    CFD_SOR_FUSED=$v timeout -k 10 300 python tools/bench_solvers.py --n 4096 --iters 200 --reps 5 > gpurun_out/pm_solvers_sor$v.log 2>&1 || { tail -5 gpurun_out/pm_solvers_sor$v.log; exit 1; }
+    echo "sor_fused=$v"; cat gpurun_out/pm_solvers_sor$v.log
+  done
+fi
 echo DONE
