@@ -68,6 +68,10 @@ constexpr int kStampWaves = 1 << 15;
 __device__ unsigned long long g_lds_stamp[kStampWaves * 4];
 #endif
 
+#ifndef CFD_LDS_HOIST
+#define CFD_LDS_HOIST 0  // 1: read a slot's T rhs rows from the LDS ring at its start (r2: 5.09 vs 5.00 us/sweep, off)
+#endif
+
 #ifndef CFD_LDS_LAG
 #define CFD_LDS_LAG 1  // rows between consecutive stages of one slot (see LdsMarch)
 #endif
@@ -176,6 +180,14 @@ struct LdsMarch {
         if (!(CFD_LDS_DIAG & 2))
             ring[(V_ % D) * 64 + lane] = make_float2(RQ[V_ % PD].x, RQ[V_ % PD].y);   // rhs row k
         RQ[V_ % PD] = ld(rs_r, k + PD);
+        // the slot's T ring reads issued together (the ring rows of earlier
+        // slots; this slot's write went to another entry): one LDS latency
+        // per slot instead of one per stage
+        float2 rhv[T];
+        if (CFD_LDS_HOIST && !(CFD_LDS_DIAG & 2)) {
+#pragma unroll
+            for (int s = 1; s <= T; ++s) rhv[s - 1] = ring[((V_ - L * s + 8 * D) % D) * 64 + lane];
+        }
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
             if (GUARD == 0 && V_ < (L + 1) * s) continue;            // compile-time
@@ -184,7 +196,8 @@ struct LdsMarch {
             const int r = k - L * s;
             const float2 rh = (CFD_LDS_DIAG & 2)
                                   ? make_float2(RQ[(V_ + s) % PD].x, RQ[(V_ + s) % PD].y)
-                                  : ring[((V_ - L * s + 8 * D) % D) * 64 + lane];
+                                  : (CFD_LDS_HOIST ? rhv[s - 1]
+                                                   : ring[((V_ - L * s + 8 * D) % D) * 64 + lane]);
             // stage s-1 finished row x at slot x - k_first + L(s-1)
             constexpr int kW = 4 * NW;
             const f2 &B = W[s - 1][(V_ - L - 1 + kW) % NW];          // stage s-1, row r-1
