@@ -201,13 +201,15 @@ constexpr int kMgMaxLevels = 40;
 void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorConst &k, int color,
                       Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
                       hipStream_t s);
-// One whole red-black iteration per launch (k_sor_fused), ping-pong between
-// pa / pb from ctl->cur (iteration `it` reads buffer (cur + it) & 1; it = 0
-// reads nothing: p' starts at 0), when sor_fused_ok(nx, ny).
-bool sor_fused_ok(int nx, int ny);
+// One whole red-black iteration per launch (k_sor_fused) over the local
+// interior rows [row_lo, row_hi) of a slab starting at global row j0 (p' and
+// rhs rows readable in [lo_clamp, hi_clamp]), ping-pong between pa / pb from
+// ctl->cur (iteration `it` reads buffer (cur + it) & 1; it = 0 reads nothing:
+// p' starts at 0), when sor_fused_ok(nx, row_hi - row_lo).
+bool sor_fused_ok(int nx, int nrows);
 void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, const SorConst &k,
                       Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
-                      hipStream_t s);
+                      int row_lo, int row_hi, int j0, int lo_clamp, int hi_clamp, hipStream_t s);
 void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
                       hipStream_t s);

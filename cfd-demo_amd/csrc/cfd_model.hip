@@ -338,24 +338,115 @@ struct cfd_model {
         timed_launches += launches;
     }
 
-    // SOR (index.html:741-774) swept red-black, in place on the current p'.
-    int enqueue_sor(int pass) {
-        const int iters = params.jacobi_iters;
-        hipEvent_t e0;
-        begin_solve_timing(pass, &e0);
+    SorConst sor_consts() const {
         SorConst k;
         double r[3];
         level_consts((double)g.dx, (double)g.dy, &k.dx2, &k.dy2, &k.denom, r, &k.fast);
         k.r_dx2 = r[0];
         k.r_dy2 = r[1];
         k.r_denom = r[2];
-        if (iters > 0 && sor_fused && sor_fused_ok(g.nx, g.ny)) {
+        return k;
+    }
+
+    // SOR on a slab (k_sor_fused over the owned interior rows): each
+    // iteration reads 2 p' ghost rows per side (the red rows just outside the
+    // slab are recomputed from them) and 1 rhs ghost row, so the written
+    // buffer's 2 boundary rows go to the neighbours after every iteration.
+    // Fixed count: only the last iteration's residual is all-reduced.  With
+    // the tolerance on (residual_out != null, the host-driven corrector loop)
+    // every iteration's is, and the host checks them one iteration behind
+    // the launches, as the sharded Jacobi does (model.rs:816 / index.html:772).
+    int enqueue_sor_sharded(const SorConst &k, int pass, float *residual_out, hipEvent_t e0) {
+        const int iters = params.jacobi_iters;
+        const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
+        if (iters < 1 || g.hg < 2 || !sor_fused_ok(g.nx, hi - lo))
+            return fail(CFD_EINVAL, "sharded SOR needs >= 1 iteration, halo depth >= 2 and >= 16 "
+                                    "interior rows per slab");
+        const bool tol = g.tol_enabled != 0;
+        float res_local = 0.f;
+        if (tol && !residual_out) residual_out = &res_local;
+        int rc = exchange(FLD_RHS, HALO_PP, 1);
+        if (rc) return rc;
+        int n = iters, checked = 0;
+        bool done = false;
+        auto converged = [&](int it, bool *yes) -> int {
+            int rc2 = wait_done(ev_res[it % kResRing]);
+            if (rc2) return rc2;
+            float e;
+            std::memcpy(&e, (const void *)&h_res[it % kResRing], 4);
+            *yes = e < params.p_tol;
+            return 0;
+        };
+        for (int it = 0; it < iters && !done; ++it) {
+            const int res = tol || it == iters - 1;
+            launch_sor_fused(f.pp[0], f.pp[1], f.rhs, g.nx, g.ny, k, f.ctl, f.err_slots, pass, it,
+                             tol, g.p_tol, res, lo, hi, (int)j0, -g.hg, g.nyl + g.hg - 1, stream);
+            if (res) {
+                launch_fold_slots(f.ctl->err + it, f.err_slots + (size_t)it * kResSlots * kResStride,
+                                  1, stream);
+                rc = allreduce_max_u32(f.ctl->err + it, 1);
+                if (rc) return rc;
+            }
+            rc = exchange_pp((host_cur + it + 1) & 1, 2);
+            if (rc) return rc;
+            if (!tol) continue;
+            HIP_TRY(hipMemcpyAsync(&h_res[it % kResRing], f.ctl->err + it, 4, hipMemcpyDeviceToHost,
+                                   stream));
+            HIP_TRY(hipEventRecord(ev_res[it % kResRing], stream));
+            while (checked <= it - 1 && !done) {
+                bool yes = false;
+                rc = converged(checked, &yes);
+                if (rc) return rc;
+                if (yes) {
+                    n = checked + 1;
+                    done = true;
+                }
+                ++checked;
+            }
+        }
+        while (tol && !done && checked < iters) {
+            bool yes = false;
+            rc = converged(checked, &yes);
+            if (rc) return rc;
+            if (yes) {
+                n = checked + 1;
+                done = true;
+            }
+            ++checked;
+        }
+        end_solve_timing(e0, (uint64_t)n, (uint64_t)n);
+        // with the tolerance on the finalize recounts n from the (identical)
+        // all-reduced residuals and flips the buffer n times
+        launch_finalize_solve(g, f, tol ? -1 : pass, iters, !tol && pass >= 1 ? 1 : 0, iters,
+                              stream);
+        HIP_TRY(hipGetLastError());
+        host_cur = (host_cur + (tol ? n : iters)) & 1;
+        pp_ghosts_shallow = true;
+        if (tol) {
+            float r = 0.f;
+            HIP_TRY(hipMemcpyAsync(&r, &f.ctl->last_p, 4, hipMemcpyDeviceToHost, stream));
+            rc = wait_done(nullptr);
+            if (rc) return rc;
+            *residual_out = r;
+        }
+        return 0;
+    }
+
+    // SOR (index.html:741-774) swept red-black: fused iterations ping-pong
+    // (sor_fused), else two color passes in place on the current p'.
+    int enqueue_sor(int pass) {
+        const int iters = params.jacobi_iters;
+        hipEvent_t e0;
+        begin_solve_timing(pass, &e0);
+        const SorConst k = sor_consts();
+        if (sharded()) return enqueue_sor_sharded(k, pass, nullptr, e0);
+        if (iters > 0 && sor_fused && sor_fused_ok(g.nx, g.ny - 2)) {
             // one launch per iteration, ping-pong from the device's current
             // buffer; the finalize flips it once per executed iteration
             for (int it = 0; it < iters; ++it)
                 launch_sor_fused(f.pp[0], f.pp[1], f.rhs, g.nx, g.ny, k, f.ctl, f.err_slots, pass,
-                                 it, g.tol_enabled, g.p_tol, g.tol_enabled || it == iters - 1,
-                                 stream);
+                                 it, g.tol_enabled, g.p_tol, g.tol_enabled || it == iters - 1, 1,
+                                 g.ny - 1, 0, -g.hg, g.nyl + g.hg - 1, stream);
             end_solve_timing(e0, (uint64_t)iters, (uint64_t)iters);
             launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, iters, stream);
             if (!g.tol_enabled) host_cur = (host_cur + iters) & 1;
@@ -595,6 +686,11 @@ struct cfd_model {
     // (k_jacobi's early exit), so p' and the sweep count are the reference's;
     // only its all-reduce and exchange of an untouched buffer run in vain.
     int enqueue_solve_host_driven(float *residual_out) {
+        if (params.pressure_solver == CFD_SOLVER_SOR) {
+            hipEvent_t e0;
+            begin_solve_timing(-1, &e0);
+            return enqueue_sor_sharded(sor_consts(), -1, residual_out, e0);
+        }
         const int iters = params.jacobi_iters;
         const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
         constexpr int kLag = 1;
@@ -1109,8 +1205,8 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     int rc = validate(grid, params);
     if (rc) return rc;
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad rank/n_ranks");
-    if (n_ranks > 1 && params->pressure_solver != CFD_SOLVER_JACOBI)
-        return fail(CFD_EINVAL, "SOR and multigrid solvers run on unsharded models only");
+    if (n_ranks > 1 && params->pressure_solver == CFD_SOLVER_MULTIGRID)
+        return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(CFD_EHIP, "no HIP device available");
@@ -1175,8 +1271,8 @@ int cfdrt_check_params(const cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
     if (rc) return rc;
-    if (m->sharded() && p->pressure_solver != CFD_SOLVER_JACOBI)
-        return fail(CFD_EINVAL, "SOR and multigrid solvers run on unsharded models only");
+    if (m->sharded() && p->pressure_solver == CFD_SOLVER_MULTIGRID)
+        return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     return 0;
 }
 
@@ -1328,8 +1424,8 @@ int cfd_set_params(cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
     if (rc) return rc;
-    if (m->sharded() && p->pressure_solver != CFD_SOLVER_JACOBI)
-        return fail(CFD_EINVAL, "SOR and multigrid solvers run on unsharded models only");
+    if (m->sharded() && p->pressure_solver == CFD_SOLVER_MULTIGRID)
+        return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     rc = m->sync();
     if (rc) return rc;
     {

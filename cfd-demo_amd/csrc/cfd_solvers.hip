@@ -96,8 +96,9 @@ __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
 // `src` and written to the other buffer, so p' and rhs cross HBM once per
 // iteration (12 B per cell-update) instead of once per color.  A wave owns 64
 // lanes x one column pair (one red and one black cell per row) and a segment
-// of R interior rows [r0, r0+R); all rows it needs — p' rows r0-2..r0+R+1 and
-// rhs rows r0-1..r0+R — are loaded up front, then
+// of R interior rows [r0, r0+R) (local rows of the model's slab; a sharded
+// slab needs 2 ghost rows of p' and 1 of rhs); all rows it needs — p' rows
+// r0-2..r0+R+1 and rhs rows r0-1..r0+R — are loaded up front, then
 //   red  rows r0-1..r0+R   from the old black neighbours (src),
 //   black rows r0..r0+R-1  from the new red ones (registers),
 // exactly the two color passes of k_sor_color over the same values: a red
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
 // Horizontal neighbours come from the adjacent lanes (DPP); lanes 0 and 63
 // only feed them, so waves step 62 pairs.  Iteration 0 reads no source: the
 // solve starts from p' = 0 (index.html:743).  The last segment of a column
-// ends at row ny-1 and overlaps its neighbour (identical stores).
+// ends at row_hi and overlaps its neighbour (identical stores).
 template <int FAST, int R>
 __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ pa,
                                                       const float *__restrict__ pb,
@@ -116,7 +117,9 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
                                                       const float *__restrict__ rhs, int nx, int ny,
                                                       SorConst k, Ctl *ctl, uint32_t *err_slots,
                                                       int pass, int it, int tol, float p_tol,
-                                                      int res, int nwc, int nseg) {
+                                                      int res, int nwc, int nseg, int row_lo,
+                                                      int row_hi, int j0, int lo_clamp,
+                                                      int hi_clamp) {
     if (pass_off(ctl, pass)) return;
     if (tol && it > 0 &&
         read_max(err_slots + (size_t)(it - 1) * kResSlots * kResStride, ctl->err[it - 1]) < p_tol)
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
     const int si = (ctl->cur + it) & 1;
     const float *__restrict__ src = si ? pb : pa;
     float *__restrict__ dst = si ? qa : qb;
-    const int r0 = 1 + min(seg * R, ny - 2 - R);
+    const int r0 = row_lo + min(seg * R, row_hi - row_lo - R);   // local rows
     const int c = wc * 62 - 1 + lane;
     const bool in_dom = c >= 0 && 2 * c < nx;
     const bool out = in_dom && lane >= 1 && lane <= 62;
@@ -139,13 +142,13 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
     float2 A[R + 4], Rh[R + 2];   // p' rows r0-2+q, rhs rows r0-1+q
 #pragma unroll
     for (int q = 0; q < R + 4; ++q) {
-        const int r = min(max(r0 - 2 + q, 0), ny - 1);
+        const int r = min(max(r0 - 2 + q, lo_clamp), hi_clamp);
         A[q] = (in_dom && it > 0) ? *reinterpret_cast<const float2 *>(src + (long)r * nx + i0)
                                   : make_float2(0.0f, 0.0f);
     }
 #pragma unroll
     for (int q = 0; q < R + 2; ++q) {
-        const int r = min(max(r0 - 1 + q, 0), ny - 1);
+        const int r = min(max(r0 - 1 + q, lo_clamp), hi_clamp);
         Rh[q] = in_dom ? *reinterpret_cast<const float2 *>(rhs + (long)r * nx + i0)
                        : make_float2(0.0f, 0.0f);
     }
@@ -167,11 +170,11 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
     float red[R + 2];
 #pragma unroll
     for (int q = 0; q < R + 2; ++q) {
-        const int r = r0 - 1 + q;   // wave-uniform
+        const int r = r0 - 1 + q;   // wave-uniform, local
         const float2 a = A[q + 1], up = A[q + 2], dn = A[q];
-        const bool row_in = r >= 1 && r <= ny - 2;
+        const bool row_in = j0 + r >= 1 && j0 + r <= ny - 2;
         const bool count = out && q >= 1 && q <= R;
-        if ((r & 1) == 0) {   // red at x (column i0)
+        if (((j0 + r) & 1) == 0) {   // red at x (column i0)
             const int i = i0;
             red[q] = relax(a.x, a.y, from_left(a.y), up.x, dn.x, Rh[q].x,
                            row_in && i >= 1 && i <= nx - 2, count);
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
         const float2 a = A[q + 2];
         const float rd = red[q + 1];
         float2 o;
-        if ((r & 1) == 0) {   // red at x, black at y (column i0 + 1)
+        if (((j0 + r) & 1) == 0) {   // red at x, black at y (column i0 + 1)
             const int i = i0 + 1;
             o.x = rd;
             o.y = relax(a.y, from_right(rd), rd, red[q + 2], red[q], Rh[q + 1].y,
@@ -203,8 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
         if (i0 + 1 == nx - 1) o.y = 0.0f;  // P(nx-1,j) = 0
         if (out) {
             *reinterpret_cast<float2 *>(dst + (long)r * nx + i0) = o;
-            if (r == 1) *reinterpret_cast<float2 *>(dst + i0) = o;                              // row 0
-            if (r == ny - 2) *reinterpret_cast<float2 *>(dst + (long)(ny - 1) * nx + i0) = o;  // row ny-1
+            if (j0 + r == 1) *reinterpret_cast<float2 *>(dst + (long)(r - 1) * nx + i0) = o;       // row 0
+            if (j0 + r == ny - 2) *reinterpret_cast<float2 *>(dst + (long)(r + 1) * nx + i0) = o;  // row ny-1
         }
     }
     if (!res) return;
@@ -525,20 +528,23 @@ void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorCons
                            k, color, ctl, err_slots, pass, it, tol, p_tol, res, nbx);
 }
 
-bool sor_fused_ok(int nx, int ny) { return nx % 2 == 0 && nx >= 4 && ny - 2 >= kSorRows; }
+bool sor_fused_ok(int nx, int nrows) { return nx % 2 == 0 && nx >= 4 && nrows >= kSorRows; }
 
 void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, const SorConst &k,
                       Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
-                      hipStream_t s) {
+                      int row_lo, int row_hi, int j0, int lo_clamp, int hi_clamp, hipStream_t s) {
     const int nwc = cdiv(nx / 2, 62);
-    const int nseg = cdiv(ny - 2, kSorRows);
+    const int nseg = cdiv(row_hi - row_lo, kSorRows);
     const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
+#define CFD_LAUNCH_SOR(FASTV)                                                                       \
+    hipLaunchKernelGGL((k_sor_fused<FASTV, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs, \
+                       nx, ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg, row_lo,      \
+                       row_hi, j0, lo_clamp, hi_clamp)
     if (k.fast)
-        hipLaunchKernelGGL((k_sor_fused<1, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs, nx,
-                           ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg);
+        CFD_LAUNCH_SOR(1);
     else
-        hipLaunchKernelGGL((k_sor_fused<0, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs, nx,
-                           ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg);
+        CFD_LAUNCH_SOR(0);
+#undef CFD_LAUNCH_SOR
 }
 
 void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s) {

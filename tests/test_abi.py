@@ -91,13 +91,14 @@ def test_invalid_arguments_rejected_before_device():
 
 
 def test_solver_choice_validated_before_device():
-    """pressure_solver 0..2; SOR / multigrid are rejected for sharded models."""
+    """pressure_solver 0..2; multigrid is rejected for sharded models (SOR
+    runs on slabs since r2, tests/test_gpu_sharded.py)."""
     import cfdamd
     with pytest.raises(cfdamd.CfdError) as e:
         cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0),
                      cfdamd.SimulationParams(pressure_solver=3))
     assert e.value.code == -1
-    for solver in (cfdamd.PressureSolver.Sor, cfdamd.PressureSolver.Multigrid):
+    for solver in (cfdamd.PressureSolver.Multigrid,):
         with pytest.raises(cfdamd.CfdError) as e:
             cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0),
                          cfdamd.SimulationParams(pressure_solver=solver),

@@ -220,3 +220,20 @@ def test_sharded_tolerance_toggle_keeps_deep_ghosts():
     got = assemble(states, 96)
     for f in FIELDS:
         assert_bitwise(f"toggle:{f}", got[f], o.field(f))
+
+
+@pytest.mark.parametrize("n,tol,depth", [(2, False, 4), (3, True, 2), (4, False, 8), (4, True, 3)])
+def test_sharded_sor_matches_oracle(n, tol, depth):
+    """SOR (pressure_solver 1, the JS variant's solver) on slabs: k_sor_fused
+    over each slab's interior rows, 2 p' ghost rows exchanged after every
+    iteration, the residual all-reduced (every iteration, host-checked one
+    iteration behind, with the tolerance on; the last one otherwise), the
+    cylinder across a slab boundary, corrector passes: bitwise against the
+    single-domain oracle."""
+    import cfdamd
+    grid = cfdamd.Grid(128, 96, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.9))
+    params = cfdamd.SimulationParams(pressure_solver=cfdamd.PressureSolver.Sor, jacobi_iters=30,
+                                     corrector_passes=3, tol_enabled=tol)
+    st = run_sharded(n, grid, params, 4, depth)
+    check_against_oracle(st, grid, dict(pressure_solver=1, jacobi_iters=30, corrector_passes=3,
+                                        tol_enabled=int(tol)), 4, FIELDS + ("rhs",))
