@@ -213,9 +213,15 @@ void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, co
 void launch_fill_zero(float *p, size_t n, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
                       hipStream_t s);
-// Five smoothing sweeps src -> dst in one launch (LDS temporal blocking).
+// Five smoothing sweeps src -> dst in one launch (temporal blocking: one
+// wave per register window, or the LDS block form with CFD_MG_SMOOTH=1).
 void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
                        hipStream_t s);
+// The wave-window form is selected (then the up-leg fuses its prolong-add
+// into the smoothing: launch_mg_prolong_smooth5 reads src + prolongate(e)).
+bool mg_smooth_wave_form();
+void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel &L, const float *src,
+                               float *dst, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_residual(const MgLevel &L, const float *p, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_restrict(const MgLevel &F, const MgLevel &Cl, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_prolong_add(const MgLevel &Cl, const float *e, const MgLevel &F, float *p,

@@ -571,7 +571,14 @@ struct cfd_model {
             ++launches;
             for (int l = mg_tail - 1; l >= 0; --l) {   // up: prolong-add into b, 5 smooths b->a
                 const MgLevel L = lvl(l), Cl = lvl(l + 1);
-                launch_mg_prolong_add(Cl, l + 1 == lc ? Cl.b : Cl.a, L, L.b, f.ctl, pass, stream);
+                const float *e = l + 1 == lc ? Cl.b : Cl.a;
+                if (tb && mg_smooth_wave_form()) {
+                    // the prolong-add happens as the smoothing loads its window
+                    launch_mg_prolong_smooth5(Cl, e, L, L.b, L.a, f.ctl, pass, stream);
+                    launches += 1;
+                    continue;
+                }
+                launch_mg_prolong_add(Cl, e, L, L.b, f.ctl, pass, stream);
                 smooth5(L, L.b, L.a);
                 launches += 1;
             }

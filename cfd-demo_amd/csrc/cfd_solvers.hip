@@ -291,9 +291,8 @@ __device__ __forceinline__ void mg_restrict_cell(const MgLevel &F, const MgLevel
 
 // mgProlongate (index.html:1398-1421) of the coarse error e, added to p
 // (:1464-1466): p = f32(p + f32(bilinear)).
-__device__ __forceinline__ void mg_prolong_add_cell(const MgLevel &Cl, const float *__restrict__ e,
-                                                    const MgLevel &F, float *__restrict__ p, int i,
-                                                    int j) {
+__device__ __forceinline__ float mg_prolong_add_val(const MgLevel &Cl, const float *__restrict__ e,
+                                                    float p_old, int i, int j) {
     const int nxc = Cl.nx, nyc = Cl.ny;
     const int j0 = j >> 1, i0 = i >> 1;
     const int j1 = min(j0 + 1, nyc - 1), i1 = min(i0 + 1, nxc - 1);
@@ -302,8 +301,14 @@ __device__ __forceinline__ void mg_prolong_add_cell(const MgLevel &Cl, const flo
                        a * (1 - b) * (double)e[(long)j0 * nxc + i1] +
                        (1 - a) * b * (double)e[(long)j1 * nxc + i0] +
                        a * b * (double)e[(long)j1 * nxc + i1];
+    return (float)((double)p_old + (double)(float)val);
+}
+
+__device__ __forceinline__ void mg_prolong_add_cell(const MgLevel &Cl, const float *__restrict__ e,
+                                                    const MgLevel &F, float *__restrict__ p, int i,
+                                                    int j) {
     const long idx = (long)j * F.nx + i;
-    p[idx] = (float)((double)p[idx] + (double)(float)val);
+    p[idx] = mg_prolong_add_val(Cl, e, p[idx], i, j);
 }
 
 // Five mgSmooth sweeps in one launch (temporal blocking): a block owns a
@@ -375,6 +380,69 @@ __global__ __launch_bounds__(kSmW) void k_mg_smooth5(MgLevel L, const float *__r
     if (col_in && x >= kSmT && x < kSmW - kSmT) {
 #pragma unroll
         for (int y = kSmT; y < kSmH - kSmT; ++y) {
+            const int gy = gy0 + y;
+            if (gy < ny) dst[(long)gy * nx + gx] = c[y];
+        }
+    }
+}
+
+// The same five sweeps with one WAVE per window (64 columns x kTH + 10 rows)
+// and no LDS: a lane owns one window column in registers (p as f32, rhs as
+// f32 — its widening to double is exact), and the old values of the
+// horizontal neighbours come from the adjacent lanes by DPP: the wave reads
+// them in the same instruction stream before any lane writes the row, which
+// is exactly the LDS copy of the previous sweep's row.  The 80 KB LDS
+// exchange of the block form held occupancy to 2 workgroups per CU; here
+// registers alone bound it.  Output: lanes kSmT..63-kSmT of the window.
+// PRO: the up-leg's prolong-add (index.html:1464-1466) is applied to the
+// window as it is loaded — src + prolongate(e) exactly as
+// mg_prolong_add_cell forms it — so the added field is never stored: one
+// grid-wide pass (read src and e, write src) less per level and cycle.
+template <int FAST, int kTH, bool PRO>
+__global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *__restrict__ src,
+                                                        float *__restrict__ dst, const Ctl *ctl,
+                                                        int pass, int nwx, int nwin, MgLevel Cl,
+                                                        const float *__restrict__ e) {
+    constexpr int kH = kTH + 2 * kSmT;   // window rows
+    constexpr int kOW = 64 - 2 * kSmT;   // output columns per window
+    if (pass_off(ctl, pass)) return;
+    const int lane = (int)threadIdx.x & 63;
+    const int win = (int)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    if (win >= nwin) return;   // wave-uniform
+    const int nx = L.nx, ny = L.ny;
+    const int gx = (win % nwx) * kOW - kSmT + lane;
+    const int gy0 = (win / nwx) * kTH - kSmT;
+    const bool col_in = gx >= 0 && gx < nx;
+    const bool bcol = gx == 0 || gx == nx - 1;
+    float c[kH], rh[kH];
+#pragma unroll
+    for (int y = 0; y < kH; ++y) {
+        const int gy = gy0 + y;
+        const bool in = col_in && gy >= 0 && gy < ny;
+        const long k = (long)gy * nx + gx;
+        c[y] = in ? (PRO ? mg_prolong_add_val(Cl, e, src[k], gx, gy) : src[k]) : 0.0f;
+        rh[y] = in ? L.rhs[k] : 0.0f;
+    }
+#pragma unroll 1
+    for (int s = 0; s < kSmT; ++s) {
+        // rows top-down in place: `below` keeps the old value of row y-1
+        double below = (double)c[0];
+#pragma unroll
+        for (int y = 1; y < kH - 1; ++y) {
+            const int gy = gy0 + y;
+            const double here = (double)c[y];
+            const float left = from_left(c[y]), right = from_right(c[y]);
+            if (!(bcol || gy <= 0 || gy >= ny - 1)) {
+                const double h = ddiv<FAST>((double)right + (double)left, L.dx2, L.r_dx2);
+                const double vt = ddiv<FAST>((double)c[y + 1] + below, L.dy2, L.r_dy2);
+                c[y] = (float)ddiv<FAST>(h + vt - (double)rh[y], L.denom, L.r_denom);
+            }
+            below = here;
+        }
+    }
+    if (col_in && lane >= kSmT && lane < 64 - kSmT) {
+#pragma unroll
+        for (int y = kSmT; y < kH - kSmT; ++y) {
             const int gy = gy0 + y;
             if (gy < ny) dst[(long)gy * nx + gx] = c[y];
         }
@@ -563,8 +631,54 @@ void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl 
         hipLaunchKernelGGL(k_mg_smooth<0>, dim3(g), dim3(kBlock), 0, s, L, src, dst, ctl, pass, nbx);
 }
 
+bool mg_smooth_wave_form() {
+    // CFD_MG_SMOOTH=1: the LDS block form; default: one wave per window
+    static const bool lds_form = [] {
+        const char *e = getenv("CFD_MG_SMOOTH");
+        return e && atoi(e) == 1;
+    }();
+    return !lds_form;
+}
+
+void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel &L, const float *src,
+                               float *dst, const Ctl *ctl, int pass, hipStream_t s) {
+    const bool big = (long)L.nx * L.ny >= (1L << 23);
+    const int nwx = cdiv(L.nx, 64 - 2 * kSmT);
+    const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+    const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
+#define CFD_LAUNCH_PSM5W(FASTV, TH) \
+    hipLaunchKernelGGL((k_mg_smooth5w<FASTV, TH, true>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, Cl, e)
+    if (L.fast && big)
+        CFD_LAUNCH_PSM5W(1, kSmTHBig);
+    else if (L.fast)
+        CFD_LAUNCH_PSM5W(1, kSmTHSmall);
+    else if (big)
+        CFD_LAUNCH_PSM5W(0, kSmTHBig);
+    else
+        CFD_LAUNCH_PSM5W(0, kSmTHSmall);
+#undef CFD_LAUNCH_PSM5W
+}
+
 void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
                        hipStream_t s) {
+    if (mg_smooth_wave_form()) {
+        const bool big = (long)L.nx * L.ny >= (1L << 23);
+        const int nwx = cdiv(L.nx, 64 - 2 * kSmT);
+        const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+        const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
+#define CFD_LAUNCH_SM5W(FASTV, TH) \
+        hipLaunchKernelGGL((k_mg_smooth5w<FASTV, TH, false>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, L, nullptr)
+        if (L.fast && big)
+            CFD_LAUNCH_SM5W(1, kSmTHBig);
+        else if (L.fast)
+            CFD_LAUNCH_SM5W(1, kSmTHSmall);
+        else if (big)
+            CFD_LAUNCH_SM5W(0, kSmTHBig);
+        else
+            CFD_LAUNCH_SM5W(0, kSmTHSmall);
+#undef CFD_LAUNCH_SM5W
+        return;
+    }
     const int nbx = cdiv(L.nx, kSmOW);
     const bool big = (long)L.nx * L.ny >= (1L << 23);
     const int nby = cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
