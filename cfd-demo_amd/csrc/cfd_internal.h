@@ -222,6 +222,10 @@ void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl
 bool mg_smooth_wave_form();
 void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel &L, const float *src,
                                float *dst, const Ctl *ctl, int pass, hipStream_t s);
+// ... and the down-leg forms the residual of its smoothed field in the same
+// launch (launch_mg_smooth5_residual: dst and L.r).
+void launch_mg_smooth5_residual(const MgLevel &L, const float *src, float *dst, const Ctl *ctl,
+                                int pass, hipStream_t s);
 void launch_mg_residual(const MgLevel &L, const float *p, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_restrict(const MgLevel &F, const MgLevel &Cl, const Ctl *ctl, int pass, hipStream_t s);
 void launch_mg_prolong_add(const MgLevel &Cl, const float *e, const MgLevel &F, float *p,

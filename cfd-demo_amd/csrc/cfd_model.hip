@@ -562,10 +562,17 @@ struct cfd_model {
         for (int cycle = 0; cycle < 3; ++cycle) {
             for (int l = 0; l < mg_tail; ++l) {   // down: 5 smooths a->b, residual, restrict
                 const MgLevel L = lvl(l);
-                smooth5(L, L.a, L.b);
-                launch_mg_residual(L, L.b, f.ctl, pass, stream);
+                if (tb && mg_smooth_wave_form()) {
+                    // the residual is formed by the smoothing launch itself
+                    launch_mg_smooth5_residual(L, L.a, L.b, f.ctl, pass, stream);
+                    launches += 1;
+                } else {
+                    smooth5(L, L.a, L.b);
+                    launch_mg_residual(L, L.b, f.ctl, pass, stream);
+                    launches += 1;
+                }
                 launch_mg_restrict(L, lvl(l + 1), f.ctl, pass, stream);
-                launches += 2;
+                launches += 1;
             }
             launch_mg_tail(mg_dev, mg_tail, lc, L0.a, L0.b, L0.fast, f.ctl, pass, stream);
             ++launches;

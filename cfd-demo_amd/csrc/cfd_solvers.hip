@@ -398,20 +398,26 @@ __global__ __launch_bounds__(kSmW) void k_mg_smooth5(MgLevel L, const float *__r
 // window as it is loaded — src + prolongate(e) exactly as
 // mg_prolong_add_cell forms it — so the added field is never stored: one
 // grid-wide pass (read src and e, write src) less per level and cycle.
-template <int FAST, int kTH, bool PRO>
+// RES: the down-leg's residual r = rhs - A p (index.html:1430-1441) of the
+// smoothed field is formed in the same launch: the window keeps one more
+// halo cell per side (kSmT + 1), so the smoothed values the residual reads
+// around the output tile are exact too, and the residual pass (read p and
+// rhs again, write r) goes.
+template <int FAST, int kTH, bool PRO, bool RES = false>
 __global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *__restrict__ src,
                                                         float *__restrict__ dst, const Ctl *ctl,
                                                         int pass, int nwx, int nwin, MgLevel Cl,
                                                         const float *__restrict__ e) {
-    constexpr int kH = kTH + 2 * kSmT;   // window rows
-    constexpr int kOW = 64 - 2 * kSmT;   // output columns per window
+    constexpr int kHL = kSmT + (RES ? 1 : 0);   // window halo
+    constexpr int kH = kTH + 2 * kHL;           // window rows
+    constexpr int kOW = 64 - 2 * kHL;           // output columns per window
     if (pass_off(ctl, pass)) return;
     const int lane = (int)threadIdx.x & 63;
     const int win = (int)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     if (win >= nwin) return;   // wave-uniform
     const int nx = L.nx, ny = L.ny;
-    const int gx = (win % nwx) * kOW - kSmT + lane;
-    const int gy0 = (win / nwx) * kTH - kSmT;
+    const int gx = (win % nwx) * kOW - kHL + lane;
+    const int gy0 = (win / nwx) * kTH - kHL;
     const bool col_in = gx >= 0 && gx < nx;
     const bool bcol = gx == 0 || gx == nx - 1;
     float c[kH], rh[kH];
@@ -440,9 +446,26 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *
             below = here;
         }
     }
-    if (col_in && lane >= kSmT && lane < 64 - kSmT) {
+    if (RES) {
+        // r of the output tile (mg_residual_cell's expression)
+        const bool out = col_in && lane >= kHL && lane < 64 - kHL;
 #pragma unroll
-        for (int y = kSmT; y < kH - kSmT; ++y) {
+        for (int y = kHL; y < kH - kHL; ++y) {
+            const int gy = gy0 + y;
+            const float left = from_left(c[y]), right = from_right(c[y]);
+            float r = 0.0f;
+            if (!(bcol || gy <= 0 || gy >= ny - 1)) {
+                const double ap = ddiv<FAST>((double)right + (double)left, L.dx2, L.r_dx2) +
+                                  ddiv<FAST>((double)c[y + 1] + (double)c[y - 1], L.dy2, L.r_dy2) -
+                                  L.denom * (double)c[y];
+                r = (float)((double)rh[y] - ap);
+            }
+            if (out && gy < ny) L.r[(long)gy * nx + gx] = r;
+        }
+    }
+    if (col_in && lane >= kHL && lane < 64 - kHL) {
+#pragma unroll
+        for (int y = kHL; y < kH - kHL; ++y) {
             const int gy = gy0 + y;
             if (gy < ny) dst[(long)gy * nx + gx] = c[y];
         }
@@ -657,6 +680,25 @@ void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel 
     else
         CFD_LAUNCH_PSM5W(0, kSmTHSmall);
 #undef CFD_LAUNCH_PSM5W
+}
+
+void launch_mg_smooth5_residual(const MgLevel &L, const float *src, float *dst, const Ctl *ctl,
+                                int pass, hipStream_t s) {
+    const bool big = (long)L.nx * L.ny >= (1L << 23);
+    const int nwx = cdiv(L.nx, 64 - 2 * (kSmT + 1));
+    const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+    const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
+#define CFD_LAUNCH_RSM5W(FASTV, TH) \
+    hipLaunchKernelGGL((k_mg_smooth5w<FASTV, TH, false, true>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, L, nullptr)
+    if (L.fast && big)
+        CFD_LAUNCH_RSM5W(1, kSmTHBig);
+    else if (L.fast)
+        CFD_LAUNCH_RSM5W(1, kSmTHSmall);
+    else if (big)
+        CFD_LAUNCH_RSM5W(0, kSmTHBig);
+    else
+        CFD_LAUNCH_RSM5W(0, kSmTHSmall);
+#undef CFD_LAUNCH_RSM5W
 }
 
 void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
