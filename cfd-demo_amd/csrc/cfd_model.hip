@@ -825,13 +825,11 @@ struct cfd_model {
     }
 
     // Model::update (model.rs:304-379).
-    int enqueue_update() {
-        if (timing) {
-            hipEvent_t e0 = take_event();
-            HIP_TRY(hipEventRecord(e0, stream));
-            step_events.push_back(e0);
-        }
-        HIP_TRY(hipEventRecord(ev_step0, stream));
+    // rec_step: record the step's GPU time for cfd_get_residuals (the last
+    // step of a cfd_update_n batch only: every event record on the stream
+    // costs the step a few microseconds of dispatch)
+    int enqueue_update(bool rec_step = true) {
+        if (rec_step) HIP_TRY(hipEventRecord(ev_step0, stream));
         const bool fused = params.corrector_passes == 0;
         launch_step_begin(g, f, fused ? 0 : 1, stream);
         int rc = exchange_uv();
@@ -844,17 +842,71 @@ struct cfd_model {
         if (rc) return rc;
         launch_step_finalize(g, f, stream);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(ev_step1, stream));
-        if (timing) {
-            hipEvent_t e1 = take_event();
-            HIP_TRY(hipEventRecord(e1, stream));
-            step_events.push_back(e1);
-            timed_steps++;
-        }
-        stepped = true;
+        if (rec_step) HIP_TRY(hipEventRecord(ev_step1, stream));
+        if (timing) timed_steps++;
+        if (rec_step) stepped = true;   // ev_step0 / ev_step1 hold a step
         return 0;
     }
     std::vector<hipEvent_t> step_events;
+
+    // ------------------------------------------------------------ hipGraph
+    // The launch sequence of a step is the same every step for an unsharded
+    // Jacobi model: every data-dependent choice (buffers, early exits, pass
+    // gating, dt) is read from Ctl on the device, so kernel arguments never
+    // change.  cfd_update_n then captures graph_steps steps once and replays
+    // the instantiated graph.  Dropped when the parameters
+    // change; not used while solve timing is on (its events are per solve).
+    // Opt-in (CFD_GRAPH=1): measured 1.2486 vs 1.2507 ms per step at 4096^2
+    // (r2, tools/graph_ab.py) — the inter-kernel gaps are not launch overhead.
+    hipGraphExec_t step_graph = nullptr;
+    int graph_cur_delta = 0;   // host_cur advance of one replay
+    int graph_steps = 4;
+    bool graph_enabled = [] {
+        const char *e = getenv("CFD_GRAPH");
+        return e && atoi(e) != 0;
+    }();
+    bool graph_ok() const {
+        return graph_enabled && !sharded() && !timing &&
+               params.pressure_solver == CFD_SOLVER_JACOBI;
+    }
+    void drop_graph() {
+        if (step_graph) (void)hipGraphExecDestroy(step_graph);
+        step_graph = nullptr;
+    }
+    int update_graph(int n) {
+        if (!step_graph) {
+            const int hc0 = host_cur;
+            HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+            int rc = 0;
+            for (int k = 0; k < graph_steps && !rc; ++k) rc = enqueue_update(false);
+            hipGraph_t graph = nullptr;
+            const hipError_t ce = hipStreamEndCapture(stream, &graph);
+            if (rc || ce != hipSuccess) {
+                if (graph) (void)hipGraphDestroy(graph);
+                host_cur = hc0;
+                return rc ? rc : fail(CFD_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+            }
+            const hipError_t ie = hipGraphInstantiate(&step_graph, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            if (ie != hipSuccess) {
+                step_graph = nullptr;
+                host_cur = hc0;
+                return fail(CFD_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+            }
+            graph_cur_delta = (host_cur - hc0) & 1;
+            host_cur = hc0;   // captured, not executed
+        }
+        int k = 0;
+        for (; k + graph_steps <= n - 1; k += graph_steps) {   // the last step stays out: it
+            HIP_TRY(hipGraphLaunch(step_graph, stream));       // records the step time
+            host_cur = (host_cur + graph_cur_delta) & 1;
+        }
+        for (; k < n; ++k) {
+            int rc = enqueue_update(k == n - 1);
+            if (rc) return rc;
+        }
+        return 0;
+    }
 
     int sync() {
         HIP_TRY(hipSetDevice(device));
@@ -882,6 +934,7 @@ struct cfd_model {
                           (void *)mg_pool, (void *)mg_dev})
             if (ptr) (void)hipFree(ptr);
         if (h_nonfinite) (void)hipHostFree(h_nonfinite);
+        drop_graph();
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (ev_step0) (void)hipEventDestroy(ev_step0);
         if (ev_step1) (void)hipEventDestroy(ev_step1);
@@ -1378,11 +1431,25 @@ int cfd_update_n(cfd_model *m, int n) {
     if (const uint32_t bad = *(volatile uint32_t *)m->h_nonfinite)
         return fail(CFD_ENONFINITE, "non-finite velocity (NaN/Inf) after step " + std::to_string(bad) +
                                         "; cfd_set_state clears it");
-    for (int k = 0; k < n; ++k) {
-        int rc = m->enqueue_update();
-        if (rc) return rc;
+    if (n <= 0) return 0;
+    // solve timing: one event pair around the whole batch for the step time
+    if (m->timing) {
+        hipEvent_t e0 = m->take_event();
+        HIP_TRY(hipEventRecord(e0, m->stream));
+        m->step_events.push_back(e0);
     }
-    return 0;
+    int rc = 0;
+    if (m->graph_ok()) {
+        rc = m->update_graph(n);
+    } else {
+        for (int k = 0; k < n && !rc; ++k) rc = m->enqueue_update(k == n - 1);
+    }
+    if (m->timing) {
+        hipEvent_t e1 = m->take_event();
+        HIP_TRY(hipEventRecord(e1, m->stream));
+        m->step_events.push_back(e1);
+    }
+    return rc;
 }
 
 int cfd_piso_step(cfd_model *m, float dt_sub) {
@@ -1442,6 +1509,7 @@ int cfd_set_params(cfd_model *m, const cfd_params *p) {
         return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     rc = m->sync();
     if (rc) return rc;
+    m->drop_graph();   // kernel arguments follow the parameters
     {
         // host mirror of the current p' buffer (the tolerance-driven Jacobi
         // solve flips it on the device); fixed-count and in-place solves use it
