@@ -215,6 +215,149 @@ __global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ 
     if (lane == 0) publish_max(err_slots + (size_t)it * kResSlots * kResStride, bid * (kBlock / 64) + wave, m);
 }
 
+// k_sor_fused as a row march: the same updates in the same order, with the
+// p' and rhs rows streamed through register rings (prefetched PD steps
+// ahead) instead of all loaded up front, so a wave holds ~30 VGPRs of rows
+// instead of ~80 and more waves share each SIMD.  Step t (0..R+1) forms the
+// red cells of row r0-1+t from p' rows r0-2+t..r0+t, then (t >= 2) the black
+// cells of row r0-2+t from the red rows of steps t-2..t and stores that row.
+template <int FAST, int R, int PD>
+struct SorMarch {
+    static constexpr int DA = 3 + PD;   // p' ring: rows a = t..t+2 in use, PD in flight
+    static constexpr int DB = 2 + PD;   // rhs ring: rows b = t-1, t in use
+    float2 AQ[DA], BQ[DB];
+    float red[3];                       // red cells of rows r0-1+t-2 .. r0-1+t (slot t % 3)
+    const float *src, *rhs;
+    float *dst;
+    int nx, ny, i0, r0, j0, lo_clamp, hi_clamp, it;
+    bool in_dom, out;
+    SorConst k;
+    float m;
+
+    __device__ __forceinline__ float2 ld(const float *p, int row, bool src_row) const {
+        row = min(max(row, lo_clamp), hi_clamp);
+        return (in_dom && (!src_row || it > 0)) ? *reinterpret_cast<const float2 *>(p + (long)row * nx + i0)
+                                                : make_float2(0.0f, 0.0f);
+    }
+    __device__ __forceinline__ float relax(float p_old_f, float pe, float pw, float pn, float ps,
+                                           float rh, bool upd, bool count) {
+        if (!upd) return p_old_f;
+        const double p_old = (double)p_old_f;
+        const double h = ddiv<FAST>((double)pe + (double)pw, k.dx2, k.r_dx2);
+        const double v = ddiv<FAST>((double)pn + (double)ps, k.dy2, k.r_dy2);
+        const double p_update = ddiv<FAST>(h + v - (double)rh, k.denom, k.r_denom);
+        const double omega = 1.7;
+        const float nv = (float)((1.0 - omega) * p_old + omega * p_update);
+        if (count) m = fmaxf(m, (float)fabs((double)nv - p_old));
+        return nv;
+    }
+    template <int T>
+    __device__ __forceinline__ void step() {
+        // red cells of row rr = r0-1+T (p' rows a = T..T+2, rhs row b = T)
+        {
+            const int rr = r0 - 1 + T;
+            const float2 dn = AQ[T % DA], a = AQ[(T + 1) % DA], up = AQ[(T + 2) % DA];
+            const float2 rh = BQ[T % DB];
+            const bool row_in = j0 + rr >= 1 && j0 + rr <= ny - 2;
+            const bool count = out && T >= 1 && T <= R;
+            if (((j0 + rr) & 1) == 0) {   // red at x (column i0)
+                const int i = i0;
+                red[T % 3] = relax(a.x, a.y, from_left(a.y), up.x, dn.x, rh.x,
+                                   row_in && i >= 1 && i <= nx - 2, count);
+            } else {                      // red at y (column i0 + 1)
+                const int i = i0 + 1;
+                red[T % 3] = relax(a.y, from_right(a.x), a.x, up.y, dn.y, rh.y,
+                                   row_in && i >= 1 && i <= nx - 2, count);
+            }
+        }
+        if constexpr (T >= 2) {
+            // black cells of row rb = r0-2+T: own old value p' row a = T, rhs b = T-1
+            const int rb = r0 - 2 + T;
+            const float2 a = AQ[T % DA];
+            const float2 rh = BQ[(T - 1) % DB];
+            const float rd = red[(T - 1) % 3], rdn = red[(T - 2) % 3], rup = red[T % 3];
+            float2 o;
+            if (((j0 + rb) & 1) == 0) {   // red at x, black at y (column i0 + 1)
+                const int i = i0 + 1;
+                o.x = rd;
+                o.y = relax(a.y, from_right(rd), rd, rup, rdn, rh.y, i >= 1 && i <= nx - 2, out);
+            } else {                      // black at x (column i0), red at y
+                const int i = i0;
+                o.y = rd;
+                o.x = relax(a.x, rd, from_left(rd), rup, rdn, rh.x, i >= 1 && i <= nx - 2, out);
+            }
+            if (i0 == 0) o.x = o.y;            // P(0,j) = P(1,j)
+            if (i0 + 1 == nx - 1) o.y = 0.0f;  // P(nx-1,j) = 0
+            if (out) {
+                *reinterpret_cast<float2 *>(dst + (long)rb * nx + i0) = o;
+                if (j0 + rb == 1) *reinterpret_cast<float2 *>(dst + (long)(rb - 1) * nx + i0) = o;       // row 0
+                if (j0 + rb == ny - 2) *reinterpret_cast<float2 *>(dst + (long)(rb + 1) * nx + i0) = o;  // row ny-1
+            }
+        }
+        // the ring slots the step is done with take the rows DA / DB ahead
+        AQ[T % DA] = ld(src, r0 - 2 + T + DA, true);
+        if constexpr (T >= 1) BQ[(T - 1) % DB] = ld(rhs, r0 - 1 + T - 1 + DB, false);
+    }
+    template <int T>
+    __device__ __forceinline__ void steps() {
+        if constexpr (T <= R + 1) {
+            step<T>();
+            steps<T + 1>();
+        }
+    }
+    __device__ __forceinline__ void run() {
+#pragma unroll
+        for (int a = 0; a < DA; ++a) AQ[a] = ld(src, r0 - 2 + a, true);
+#pragma unroll
+        for (int b = 0; b < DB; ++b) BQ[b] = ld(rhs, r0 - 1 + b, false);
+        steps<0>();
+    }
+};
+
+template <int FAST, int R>
+__global__ __launch_bounds__(kBlock) void k_sor_march(const float *__restrict__ pa,
+                                                      const float *__restrict__ pb,
+                                                      float *__restrict__ qa, float *__restrict__ qb,
+                                                      const float *__restrict__ rhs, int nx, int ny,
+                                                      SorConst k, Ctl *ctl, uint32_t *err_slots,
+                                                      int pass, int it, int tol, float p_tol,
+                                                      int res, int nwc, int nseg, int row_lo,
+                                                      int row_hi, int j0, int lo_clamp,
+                                                      int hi_clamp) {
+    if (pass_off(ctl, pass)) return;
+    if (tol && it > 0 &&
+        read_max(err_slots + (size_t)(it - 1) * kResSlots * kResStride, ctl->err[it - 1]) < p_tol)
+        return;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int lane = (int)threadIdx.x & 63;
+    const int bid = (int)blockIdx.x;
+    const int wc = bid % nwc;
+    const int seg = (bid / nwc) * (kBlock / 64) + wave;
+    if (seg >= nseg) return;   // wave-uniform
+    SorMarch<FAST, R, 2> w;
+    const int si = (ctl->cur + it) & 1;
+    w.src = si ? pb : pa;
+    w.dst = si ? qa : qb;
+    w.rhs = rhs;
+    w.nx = nx;
+    w.ny = ny;
+    w.r0 = row_lo + min(seg * R, row_hi - row_lo - R);
+    w.j0 = j0;
+    w.lo_clamp = lo_clamp;
+    w.hi_clamp = hi_clamp;
+    w.it = it;
+    const int c = wc * 62 - 1 + lane;
+    w.in_dom = c >= 0 && 2 * c < nx;
+    w.out = w.in_dom && lane >= 1 && lane <= 62;
+    w.i0 = 2 * c;
+    w.k = k;
+    w.m = 0.0f;
+    w.run();
+    if (!res) return;
+    const float m = wave_max(w.out ? w.m : 0.0f);
+    if (lane == 0) publish_max(err_slots + (size_t)it * kResSlots * kResStride, bid * (kBlock / 64) + wave, m);
+}
+
 // p' = 0 at the start of a solve (index.html:743, :777), gated by the
 // corrector loop like every solve kernel.
 __global__ __launch_bounds__(kBlock) void k_fill_zero(float4 *p, long n4, const Ctl *ctl, int pass) {
@@ -595,7 +738,10 @@ __global__ __launch_bounds__(kBlock) void k_mg_final_residual(MgLevel L, const f
     }
 }
 
-constexpr int kSorRows = 16;   // interior rows per k_sor_fused segment
+#ifndef CFD_SOR_ROWS
+#define CFD_SOR_ROWS 16
+#endif
+constexpr int kSorRows = CFD_SOR_ROWS;   // interior rows per k_sor_fused / k_sor_march segment
 
 inline int grid_of(int nx, int ny, int *nbx) {
     *nbx = cdiv(nx, kBlock);
@@ -627,14 +773,26 @@ void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, co
     const int nwc = cdiv(nx / 2, 62);
     const int nseg = cdiv(row_hi - row_lo, kSorRows);
     const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
-#define CFD_LAUNCH_SOR(FASTV)                                                                       \
-    hipLaunchKernelGGL((k_sor_fused<FASTV, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs, \
+    // CFD_SOR_MARCH=0: the all-rows-up-front form
+    static const bool march = [] {
+        const char *e = getenv("CFD_SOR_MARCH");
+        return !(e && atoi(e) == 0);
+    }();
+#define CFD_LAUNCH_SOR(KER, FASTV)                                                                  \
+    hipLaunchKernelGGL((KER<FASTV, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs,        \
                        nx, ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg, row_lo,      \
                        row_hi, j0, lo_clamp, hi_clamp)
-    if (k.fast)
-        CFD_LAUNCH_SOR(1);
-    else
-        CFD_LAUNCH_SOR(0);
+    if (march) {
+        if (k.fast)
+            CFD_LAUNCH_SOR(k_sor_march, 1);
+        else
+            CFD_LAUNCH_SOR(k_sor_march, 0);
+    } else {
+        if (k.fast)
+            CFD_LAUNCH_SOR(k_sor_fused, 1);
+        else
+            CFD_LAUNCH_SOR(k_sor_fused, 0);
+    }
 #undef CFD_LAUNCH_SOR
 }
 
