@@ -738,10 +738,10 @@ __global__ __launch_bounds__(kBlock) void k_mg_final_residual(MgLevel L, const f
     }
 }
 
-#ifndef CFD_SOR_ROWS
-#define CFD_SOR_ROWS 16
-#endif
-constexpr int kSorRows = CFD_SOR_ROWS;   // interior rows per k_sor_fused / k_sor_march segment
+// interior rows per k_sor_fused / k_sor_march segment: 32 where the slab has
+// them (4096^2, 200 iterations: 9.02 ms; 8 rows 9.60, 16 rows 9.94, 64 rows
+// 13.45), else 16 (the minimum: sor_fused_ok)
+constexpr int kSorRows = 16, kSorRowsBig = 32;
 
 inline int grid_of(int nx, int ny, int *nbx) {
     *nbx = cdiv(nx, kBlock);
@@ -771,27 +771,36 @@ void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, co
                       Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
                       int row_lo, int row_hi, int j0, int lo_clamp, int hi_clamp, hipStream_t s) {
     const int nwc = cdiv(nx / 2, 62);
-    const int nseg = cdiv(row_hi - row_lo, kSorRows);
-    const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
+    const bool big = row_hi - row_lo >= kSorRowsBig;
+    int nseg = cdiv(row_hi - row_lo, big ? kSorRowsBig : kSorRows);
+    dim3 grid(nwc * cdiv(nseg, kBlock / 64));
     // CFD_SOR_MARCH=0: the all-rows-up-front form
     static const bool march = [] {
         const char *e = getenv("CFD_SOR_MARCH");
         return !(e && atoi(e) == 0);
     }();
-#define CFD_LAUNCH_SOR(KER, FASTV)                                                                  \
-    hipLaunchKernelGGL((KER<FASTV, kSorRows>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs,        \
+#define CFD_LAUNCH_SOR(KER, FASTV, RR)                                                              \
+    hipLaunchKernelGGL((KER<FASTV, RR>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs,              \
                        nx, ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg, row_lo,      \
                        row_hi, j0, lo_clamp, hi_clamp)
     if (march) {
-        if (k.fast)
-            CFD_LAUNCH_SOR(k_sor_march, 1);
+        if (k.fast && big)
+            CFD_LAUNCH_SOR(k_sor_march, 1, kSorRowsBig);
+        else if (k.fast)
+            CFD_LAUNCH_SOR(k_sor_march, 1, kSorRows);
+        else if (big)
+            CFD_LAUNCH_SOR(k_sor_march, 0, kSorRowsBig);
         else
-            CFD_LAUNCH_SOR(k_sor_march, 0);
+            CFD_LAUNCH_SOR(k_sor_march, 0, kSorRows);
     } else {
+        // the all-rows-up-front form keeps 16-row segments
+        const int nseg16 = cdiv(row_hi - row_lo, kSorRows);
+        nseg = nseg16;
+        grid = dim3(nwc * cdiv(nseg, kBlock / 64));
         if (k.fast)
-            CFD_LAUNCH_SOR(k_sor_fused, 1);
+            CFD_LAUNCH_SOR(k_sor_fused, 1, kSorRows);
         else
-            CFD_LAUNCH_SOR(k_sor_fused, 0);
+            CFD_LAUNCH_SOR(k_sor_fused, 0, kSorRows);
     }
 #undef CFD_LAUNCH_SOR
 }
