@@ -478,7 +478,10 @@ struct cfd_model {
             dims.push_back({(dims.back().first + 1) / 2, (dims.back().second + 1) / 2});
         }
         const int nl = (int)dims.size();
-        size_t total = round4((size_t)g.nx * g.ny);   // level-0 residual
+        // level 0: the residual; a sharded model also keeps full-grid
+        // solution buffers and the gathered rhs (every rank solves the whole
+        // grid redundantly, see enqueue_mg)
+        size_t total = (sharded() ? 4 : 1) * round4((size_t)g.nx * g.ny);
         for (int l = 1; l < nl; ++l) total += 4 * round4((size_t)dims[l].first * dims[l].second);
         HIP_TRY(hipMalloc((void **)&mg_pool, total * 4));
         HIP_TRY(hipMemsetAsync(mg_pool, 0, total * 4, stream));
@@ -495,7 +498,12 @@ struct cfd_model {
             L.nx = dims[l].first;
             L.ny = dims[l].second;
             const size_t n = (size_t)L.nx * L.ny;
-            if (l == 0) {
+            if (l == 0 && sharded()) {
+                L.a = take(n);
+                L.b = take(n);
+                L.rhs = take(n);
+                L.r = take(n);
+            } else if (l == 0) {
                 L.rhs = f.rhs;
                 L.r = take(n);
             } else {
@@ -528,15 +536,52 @@ struct cfd_model {
 
     // The multigrid branch (index.html:775-795): p' = 0, 3 V-cycles on the
     // current p' buffer, residual max |A p' - rhs| into the solve's slot set.
-    int enqueue_mg(int pass) {
+    // Sharded multigrid: the V-cycle's coarse levels shrink below one row per
+    // slab, so every rank gathers the whole rhs (point-to-point all-gather),
+    // solves the whole grid redundantly with the single-domain kernels — the
+    // same arithmetic on the same data, so every rank holds the single-domain
+    // result bit for bit — and keeps its slab's rows plus hg ghost rows of it.
+    int gather_rhs() {
+        float *full = mg[0].rhs;
+        const size_t nx = (size_t)g.nx;
+        if (hub) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();   // every member's rhs is final
+            for (cfd_model *peer : hub->members)
+                HIP_TRY(hipMemcpyAsync(full + (size_t)peer->j0 * nx, peer->f.rhs,
+                                       (size_t)peer->g.nyl * nx * 4, hipMemcpyDeviceToDevice, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();   // nobody overwrites an rhs a peer is still copying
+            return 0;
+        }
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        HIP_TRY(hipMemcpyAsync(full + (size_t)j0 * nx, f.rhs, (size_t)g.nyl * nx * 4,
+                               hipMemcpyDeviceToDevice, stream));
+        RCCL_TRY(ncclGroupStart());
+        for (int r = 0; r < n_ranks; ++r) {
+            if (r == rank) continue;
+            uint64_t a, b;
+            plan_slab(g.ny, n_ranks, r, &a, &b);
+            RCCL_TRY(ncclSend(f.rhs, (size_t)g.nyl * nx, ncclFloat, r, comm, stream));
+            RCCL_TRY(ncclRecv(full + a * nx, (size_t)(b - a) * nx, ncclFloat, r, comm, stream));
+        }
+        RCCL_TRY(ncclGroupEnd());
+        return 0;
+    }
+
+    int enqueue_mg(int pass, float *residual_out = nullptr) {
         int rc = mg_build();
         if (rc) return rc;
         hipEvent_t e0;
         begin_solve_timing(pass, &e0);
+        if (sharded()) {
+            rc = gather_rhs();
+            if (rc) return rc;
+        }
         const int lc = (int)mg.size() - 1;
         auto lvl = [&](int l) {
             MgLevel L = mg[l];
-            if (l == 0) {
+            if (l == 0 && !sharded()) {
                 L.a = f.pp[host_cur];
                 L.b = f.pp[host_cur ^ 1];
             }
@@ -591,9 +636,24 @@ struct cfd_model {
             }
         }
         launch_mg_final_residual(L0, L0.a, f.err_slots, f.ctl, pass, stream);
+        if (sharded()) {
+            // the slab's rows and its hg ghost rows (inside the grid) of the
+            // whole-grid solution: the deep ghosts are exact afterwards
+            const int lo = std::max(-g.hg, -(int)j0), hi = std::min(g.nyl + g.hg, g.ny - (int)j0);
+            HIP_TRY(hipMemcpyAsync(f.pp[host_cur] + (long)lo * g.nx, L0.a + ((long)j0 + lo) * g.nx,
+                                   (size_t)(hi - lo) * g.nx * 4, hipMemcpyDeviceToDevice, stream));
+            pp_ghosts_shallow = false;
+        }
         end_solve_timing(e0, 1, (uint64_t)launches + 1);
         launch_finalize_solve(g, f, pass, 1, pass >= 1 ? 1 : 0, 0, stream, 1);
         HIP_TRY(hipGetLastError());
+        if (residual_out) {
+            float r = 0.f;
+            HIP_TRY(hipMemcpyAsync(&r, &f.ctl->last_p, 4, hipMemcpyDeviceToHost, stream));
+            rc = wait_done(nullptr);
+            if (rc) return rc;
+            *residual_out = r;
+        }
         return 0;
     }
 
@@ -704,6 +764,10 @@ struct cfd_model {
             hipEvent_t e0;
             begin_solve_timing(-1, &e0);
             return enqueue_sor_sharded(sor_consts(), -1, residual_out, e0);
+        }
+        if (params.pressure_solver == CFD_SOLVER_MULTIGRID) {
+            float r = 0.f;
+            return enqueue_mg(-1, residual_out ? residual_out : &r);
         }
         const int iters = params.jacobi_iters;
         const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
@@ -1272,8 +1336,6 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     int rc = validate(grid, params);
     if (rc) return rc;
     if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad rank/n_ranks");
-    if (n_ranks > 1 && params->pressure_solver == CFD_SOLVER_MULTIGRID)
-        return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(CFD_EHIP, "no HIP device available");
@@ -1338,8 +1400,6 @@ int cfdrt_check_params(const cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
     if (rc) return rc;
-    if (m->sharded() && p->pressure_solver == CFD_SOLVER_MULTIGRID)
-        return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     return 0;
 }
 
@@ -1505,8 +1565,6 @@ int cfd_set_params(cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
     if (rc) return rc;
-    if (m->sharded() && p->pressure_solver == CFD_SOLVER_MULTIGRID)
-        return fail(CFD_EINVAL, "the multigrid solver runs on unsharded models only");
     rc = m->sync();
     if (rc) return rc;
     m->drop_graph();   // kernel arguments follow the parameters

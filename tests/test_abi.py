@@ -91,16 +91,14 @@ def test_invalid_arguments_rejected_before_device():
 
 
 def test_solver_choice_validated_before_device():
-    """pressure_solver 0..2; multigrid is rejected for sharded models (SOR
-    runs on slabs since r2, tests/test_gpu_sharded.py)."""
+    """pressure_solver 0..2 (all three run on slabs since r2:
+    tests/test_gpu_sharded.py); anything else is rejected before the device."""
     import cfdamd
     with pytest.raises(cfdamd.CfdError) as e:
         cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0),
                      cfdamd.SimulationParams(pressure_solver=3))
     assert e.value.code == -1
-    for solver in (cfdamd.PressureSolver.Multigrid,):
-        with pytest.raises(cfdamd.CfdError) as e:
-            cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0),
-                         cfdamd.SimulationParams(pressure_solver=solver),
-                         n_ranks=2, rank=0, unique_id=bytes(128))
-        assert e.value.code == -1 and "unsharded" in str(e.value)
+    with pytest.raises(cfdamd.CfdError) as e:
+        cfdamd.Model(cfdamd.Grid(64, 32, 1.0, 1.0), cfdamd.SimulationParams(pressure_solver=-1),
+                     n_ranks=2, rank=0, unique_id=bytes(128))
+    assert e.value.code == -1

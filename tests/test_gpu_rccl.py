@@ -24,3 +24,14 @@ def test_rccl_two_ranks_bitwise_single_domain():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert r.returncode == 0 and len(lines) == 2, (r.stdout[-2000:], r.stderr[-3000:])
     assert all(x["bitwise_equal_single_domain"] for x in lines), lines
+
+
+def test_rccl_two_ranks_solvers_bitwise_single_domain():
+    """SOR and multigrid on two RCCL ranks (socket transport on one GPU), with
+    the tolerance off and on: the gathered slabs equal a single-domain model."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_loopback.py"),
+                        "--n", "2", "--steps", "3", "--mode", "solvers"], capture_output=True,
+                       text=True, timeout=300)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 4, (r.stdout[-2000:], r.stderr[-3000:])
+    assert all(x["bitwise_equal_single_domain"] for x in lines), lines

@@ -47,6 +47,17 @@ def worker(args):
         cases.append(("channel with cylinder, reference tolerance mode (lagged convergence)",
                       cfdamd.Grid(args.nx, args.ny, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5)),
                       cfdamd.SimulationParams()))
+    if args.mode == "solvers":
+        # the JS variant's solvers on slabs: SOR (2-row exchange every
+        # iteration, all-reduced residuals) and multigrid (rhs all-gathered by
+        # point-to-point sends, whole grid solved on every rank)
+        for solver, label in ((cfdamd.PressureSolver.Sor, "SOR"),
+                              (cfdamd.PressureSolver.Multigrid, "multigrid")):
+            for tol in (False, True):
+                cases.append((f"channel with cylinder, {label}, tolerance {'on' if tol else 'off'}",
+                              cfdamd.Grid(args.nx, args.ny, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5)),
+                              cfdamd.SimulationParams(pressure_solver=solver, jacobi_iters=40,
+                                                      corrector_passes=2, tol_enabled=tol)))
     report = []
     for name, grid, params in cases:
         if rank == 0:
@@ -103,7 +114,7 @@ def main():
     ap.add_argument("--nx", type=int, default=256)
     ap.add_argument("--ny", type=int, default=200)
     ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--mode", default="both", choices=["fixed", "tol", "both"])
+    ap.add_argument("--mode", default="both", choices=["fixed", "tol", "both", "solvers"])
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
