@@ -76,33 +76,37 @@ def cpu_threads():
         return 1
 
 
-def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=3):
+def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=5):
     """The oracle (scalar/auto-vectorised C restatement) on the same workload,
     started from the GPU model's final state (so it sweeps the same developed,
     mostly non-zero fields, subnormals included, as the reference would).
     threads=1 is the reference's single worker thread (model.rs:1287);
     threads>1 splits the row loops over OpenMP threads, bit-identical results
-    (oracle/cfd_oracle.h orc_set_threads)."""
+    (oracle/cfd_oracle.h orc_set_threads).  SURVEY.md §8(d): median of the
+    per-step times of up to max_steps steps (stopping early only when the
+    budget runs out) after 1 warm-up step."""
     m, orc = oracle_from_state(nx, ny, iters, re, state, threads)
     m.update()   # untimed warm-up step: touches every page
-    steps, t0 = 0, time.perf_counter()
+    times, t_start = [], time.perf_counter()
     while True:
+        t0 = time.perf_counter()
         m.update()
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or steps >= max_steps:
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start >= budget_s or len(times) >= max_steps:
             break
     orc.set_threads(1)
     model, ncpu = cpu_info()
-    return {"value": nx * ny * iters * steps / el, "unit": "cell-updates/s", "cores": threads,
+    med = sorted(times)[len(times) // 2]
+    return {"value": nx * ny * iters / med, "unit": "cell-updates/s", "cores": threads,
             "kind": "port",
-            "sample": f"{steps} full update() step(s) of the same {nx}x{ny} cavity "
+            "sample": f"median of {len(times)} full update() step(s) of the same {nx}x{ny} cavity "
                       f"({iters} sweeps/step) from the GPU run's final state (step "
                       f"{state['simulation_step']}) after 1 warm-up step, oracle/cfd_oracle.c, "
                       f"{threads} thread(s)"
                       + (" (the reference's single worker thread)" if threads == 1 else
                          " (OpenMP row split, same bits)")
-                      + f"; ms/step {1e3 * el / steps:.0f}; host {model}, {ncpu} cpus"}
+                      + f"; ms/step median {1e3 * med:.0f} (min {1e3 * min(times):.0f}, max "
+                        f"{1e3 * max(times):.0f}); host {model}, {ncpu} cpus"}
 
 
 def oracle_from_state(nx, ny, iters, re, state, threads):
@@ -232,7 +236,7 @@ def main():
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--clock-warmup", type=float, default=0.0,
                     help="seconds of steps on a scratch model before the measured one is "
                          "created, so the GPU clocks have left their idle state")
@@ -350,6 +354,16 @@ def main():
             },
             "roofline": roof,
             "solve_fraction_of_step": tm["solve_ms"] / tm["step_ms"] if tm["step_ms"] else None,
+            # a timed-mode step moves 2,498 B per pressure cell
+            # when every pass streams its fields (P = 1 solve, K = 200 sweeps);
+            # that byte count over the measured step time, against the HBM peak
+            # (above 1 = on-chip temporal blocking, not a roofline fraction)
+            "step_algorithmic": {
+                "bytes_per_cell": 16 + 26 + 12 + 28 + 12 * args.iters + 16,
+                "GBps": (16 + 26 + 12 + 28 + 12 * args.iters + 16) * nx * ny /
+                        (elapsed / args.steps) / 1e9,
+                "x_hbm_peak": (16 + 26 + 12 + 28 + 12 * args.iters + 16) * nx * ny /
+                              (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS},
             "final_step": int(state["simulation_step"]), "final_dt": float(state["dt"]),
             "fields_finite": finite and res is not None,
         }
@@ -370,7 +384,7 @@ def main():
                 # the same restatement over all of this job's host cores
                 out["cpu_baseline_multicore"] = cpu_baseline(
                     nx, ny, args.iters, args.re, args.cpu_budget / 2, state, threads=nt,
-                    max_steps=20)
+                    max_steps=9)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -907,11 +907,87 @@ __device__ __forceinline__ float cf_u_face(const Geom &g, float inlet, float dt,
 // Same values and maxima as k_correct_finish (one float per thread held the
 // kernel near 4.7 TB/s, like the divergence before it went to float4).
 // Requires 16-byte aligned p', p, v*, v (checked by the launcher).
+// One row of k_correct_finish4's work for the 4 columns i0..i0+3 of local
+// row lj: pc = p' row lj, pb = p' row lj-1 (loaded by the caller), the step
+// maxima and the non-finite flag accumulate into du..bad.
+template <int SP>
+__device__ __forceinline__ void cf4_row(const Geom &g, const Fields &f, const float *__restrict__ pp,
+                                        float inlet, float dt, int i0, int lj, const float4 &pc,
+                                        const float4 &pb, float &du, float &dv, float &mu,
+                                        float &mv, bool &bad) {
+    const int nx = g.nx, W = nx + 1;
+    const int j = g.j0 + lj;
+    const long rp = (long)lj * nx + i0;
+    const bool vrow = (j != 0 && j != g.ny);
+    if (lj < g.nyl) {
+        const long k = (long)lj * W + i0;
+        const float pl = (i0 > 0) ? pp[rp - 1] : 0.0f;
+        const float s0 = f.u_star[k], s1 = f.u_star[k + 1], s2 = f.u_star[k + 2],
+                    s3 = f.u_star[k + 3];
+        float n0 = cf_u_face<SP>(g, inlet, dt, i0, j, s0, pc.x, pl);
+        float n1 = cf_u_face<SP>(g, inlet, dt, i0 + 1, j, s1, pc.y, pc.x);
+        float n2 = cf_u_face<SP>(g, inlet, dt, i0 + 2, j, s2, pc.z, pc.y);
+        float n3 = cf_u_face<SP>(g, inlet, dt, i0 + 3, j, s3, pc.w, pc.z);
+        if (f.n_obs > 0) {
+            if (f.mask_u[k] & 2) n0 = 0.0f;
+            if (f.mask_u[k + 1] & 2) n1 = 0.0f;
+            if (f.mask_u[k + 2] & 2) n2 = 0.0f;
+            if (f.mask_u[k + 3] & 2) n3 = 0.0f;
+        }
+        const float o0 = f.u[k], o1 = f.u[k + 1], o2 = f.u[k + 2], o3 = f.u[k + 3];
+        f.u[k] = n0;
+        f.u[k + 1] = n1;
+        f.u[k + 2] = n2;
+        f.u[k + 3] = n3;
+        du = fmaxf(fmaxf(fmaxf(du, fabsf(n0 - o0)), fmaxf(fabsf(n1 - o1), fabsf(n2 - o2))),
+                   fabsf(n3 - o3));
+        mu = fmaxf(fmaxf(fmaxf(mu, fabsf(n0)), fmaxf(fabsf(n1), fabsf(n2))), fabsf(n3));
+        bad |= nonfinite(n0) || nonfinite(n1) || nonfinite(n2) || nonfinite(n3);
+        if (i0 + 4 == nx) {   // outflow face nx copies the corrected face nx-1 (Q9)
+            float n4 = cf_u_face<SP>(g, inlet, dt, nx, j, s3, pc.w, pc.z);
+            if (f.n_obs > 0 && (f.mask_u[k + 4] & 2)) n4 = 0.0f;
+            const float o4 = f.u[k + 4];
+            f.u[k + 4] = n4;
+            du = fmaxf(du, fabsf(n4 - o4));
+            mu = fmaxf(mu, fabsf(n4));
+            bad |= nonfinite(n4);
+        }
+    }
+    float4 nv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vrow) {
+        const float4 vs = *reinterpret_cast<const float4 *>(f.v_star + rp);
+        nv.x = vs.x - dt * sdiv<SP>(pc.x - pb.x, g.dy, g.r_dy);
+        nv.y = vs.y - dt * sdiv<SP>(pc.y - pb.y, g.dy, g.r_dy);
+        nv.z = vs.z - dt * sdiv<SP>(pc.z - pb.z, g.dy, g.r_dy);
+        nv.w = vs.w - dt * sdiv<SP>(pc.w - pb.w, g.dy, g.r_dy);
+    }
+    if (f.n_obs > 0) {
+        if (f.mask_v[rp] & 2) nv.x = 0.0f;
+        if (f.mask_v[rp + 1] & 2) nv.y = 0.0f;
+        if (f.mask_v[rp + 2] & 2) nv.z = 0.0f;
+        if (f.mask_v[rp + 3] & 2) nv.w = 0.0f;
+    }
+    const float4 ov = *reinterpret_cast<const float4 *>(f.v + rp);
+    *reinterpret_cast<float4 *>(f.v + rp) = nv;
+    dv = fmaxf(fmaxf(fmaxf(dv, fabsf(nv.x - ov.x)), fmaxf(fabsf(nv.y - ov.y), fabsf(nv.z - ov.z))),
+               fabsf(nv.w - ov.w));
+    mv = fmaxf(fmaxf(fmaxf(mv, fabsf(nv.x)), fmaxf(fabsf(nv.y), fabsf(nv.z))), fabsf(nv.w));
+    bad |= nonfinite(nv.x) || nonfinite(nv.y) || nonfinite(nv.z) || nonfinite(nv.w);
+    if (lj < g.nyl) {
+        float4 p = *reinterpret_cast<const float4 *>(f.p + rp);
+        p.x = p.x + pc.x;
+        p.y = p.y + pc.y;
+        p.z = p.z + pc.z;
+        p.w = p.w + pc.w;
+        *reinterpret_cast<float4 *>(f.p + rp) = p;
+    }
+}
+
 template <int SP>
 __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, float dt_override,
                                                             int nbx) {
     Ctl *c = f.ctl;
-    const int nx = g.nx, W = nx + 1;
+    const int nx = g.nx;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
     bool bad = false;
     const long ntiles = (long)nbx * (g.nyl + 1);
@@ -927,70 +1003,64 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
         const int j = g.j0 + lj;
         const long rp = (long)lj * nx + i0;
         const bool vrow = (j != 0 && j != g.ny);
-        float4 pc = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 pc = make_float4(0.f, 0.f, 0.f, 0.f), pb = pc;
         if (lj < g.nyl || vrow) pc = *reinterpret_cast<const float4 *>(pp + rp);
-        if (lj < g.nyl) {
-            const long k = (long)lj * W + i0;
-            const float pl = (i0 > 0) ? pp[rp - 1] : 0.0f;
-            const float s0 = f.u_star[k], s1 = f.u_star[k + 1], s2 = f.u_star[k + 2],
-                        s3 = f.u_star[k + 3];
-            float n0 = cf_u_face<SP>(g, inlet, dt, i0, j, s0, pc.x, pl);
-            float n1 = cf_u_face<SP>(g, inlet, dt, i0 + 1, j, s1, pc.y, pc.x);
-            float n2 = cf_u_face<SP>(g, inlet, dt, i0 + 2, j, s2, pc.z, pc.y);
-            float n3 = cf_u_face<SP>(g, inlet, dt, i0 + 3, j, s3, pc.w, pc.z);
-            if (f.n_obs > 0) {
-                if (f.mask_u[k] & 2) n0 = 0.0f;
-                if (f.mask_u[k + 1] & 2) n1 = 0.0f;
-                if (f.mask_u[k + 2] & 2) n2 = 0.0f;
-                if (f.mask_u[k + 3] & 2) n3 = 0.0f;
-            }
-            const float o0 = f.u[k], o1 = f.u[k + 1], o2 = f.u[k + 2], o3 = f.u[k + 3];
-            f.u[k] = n0;
-            f.u[k + 1] = n1;
-            f.u[k + 2] = n2;
-            f.u[k + 3] = n3;
-            du = fmaxf(fmaxf(fmaxf(du, fabsf(n0 - o0)), fmaxf(fabsf(n1 - o1), fabsf(n2 - o2))),
-                       fabsf(n3 - o3));
-            mu = fmaxf(fmaxf(fmaxf(mu, fabsf(n0)), fmaxf(fabsf(n1), fabsf(n2))), fabsf(n3));
-            bad |= nonfinite(n0) || nonfinite(n1) || nonfinite(n2) || nonfinite(n3);
-            if (i0 + 4 == nx) {   // outflow face nx copies the corrected face nx-1 (Q9)
-                float n4 = cf_u_face<SP>(g, inlet, dt, nx, j, s3, pc.w, pc.z);
-                if (f.n_obs > 0 && (f.mask_u[k + 4] & 2)) n4 = 0.0f;
-                const float o4 = f.u[k + 4];
-                f.u[k + 4] = n4;
-                du = fmaxf(du, fabsf(n4 - o4));
-                mu = fmaxf(mu, fabsf(n4));
-                bad |= nonfinite(n4);
-            }
+        if (vrow) pb = *reinterpret_cast<const float4 *>(pp + rp - nx);
+        cf4_row<SP>(g, f, pp, inlet, dt, i0, lj, pc, pb, du, dv, mu, mv, bad);
+    }
+    flag_nonfinite(c, bad);
+    __shared__ float red[kBlock / 64][4];
+    du = wave_max(du);
+    dv = wave_max(dv);
+    mu = wave_max(mu);
+    mv = wave_max(mv);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[wv][0] = du;
+        red[wv][1] = dv;
+        red[wv][2] = mu;
+        red[wv][3] = mv;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        float r = 0.f;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) r = fmaxf(r, red[w][threadIdx.x]);
+        publish_max(f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride, bid, r);
+    }
+}
+
+// k_correct_finish4 with a thread marching down a band of kCfRows rows of its
+// 4 columns: p' row lj, loaded for row lj, is row lj+1's lower neighbour (the
+// v correction's p'(j-1)), so every p' row crosses HBM once instead of twice.
+constexpr int kCfRows = 16;
+template <int SP>
+__global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, float dt_override,
+                                                             int nbx) {
+    Ctl *c = f.ctl;
+    const int nx = g.nx;
+    float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
+    bool bad = false;
+    const int bid = xcd_block(g);
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
+    const int l0 = (bid / nbx) * kCfRows, l1 = min(l0 + kCfRows, g.nyl + 1);
+    const float dt = dt_of(c, dt_override);
+    const float inlet = c->inlet;
+    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+    if (i0 < nx) {
+        float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
+        {
+            const int j = g.j0 + l0;
+            if (j != 0 && j != g.ny) pb = *reinterpret_cast<const float4 *>(pp + (long)(l0 - 1) * nx + i0);
         }
-        float4 nv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (vrow) {
-            const float4 pb = *reinterpret_cast<const float4 *>(pp + rp - nx);
-            const float4 vs = *reinterpret_cast<const float4 *>(f.v_star + rp);
-            nv.x = vs.x - dt * sdiv<SP>(pc.x - pb.x, g.dy, g.r_dy);
-            nv.y = vs.y - dt * sdiv<SP>(pc.y - pb.y, g.dy, g.r_dy);
-            nv.z = vs.z - dt * sdiv<SP>(pc.z - pb.z, g.dy, g.r_dy);
-            nv.w = vs.w - dt * sdiv<SP>(pc.w - pb.w, g.dy, g.r_dy);
-        }
-        if (f.n_obs > 0) {
-            if (f.mask_v[rp] & 2) nv.x = 0.0f;
-            if (f.mask_v[rp + 1] & 2) nv.y = 0.0f;
-            if (f.mask_v[rp + 2] & 2) nv.z = 0.0f;
-            if (f.mask_v[rp + 3] & 2) nv.w = 0.0f;
-        }
-        const float4 ov = *reinterpret_cast<const float4 *>(f.v + rp);
-        *reinterpret_cast<float4 *>(f.v + rp) = nv;
-        dv = fmaxf(fmaxf(fmaxf(dv, fabsf(nv.x - ov.x)), fmaxf(fabsf(nv.y - ov.y), fabsf(nv.z - ov.z))),
-                   fabsf(nv.w - ov.w));
-        mv = fmaxf(fmaxf(fmaxf(mv, fabsf(nv.x)), fmaxf(fabsf(nv.y), fabsf(nv.z))), fabsf(nv.w));
-        bad |= nonfinite(nv.x) || nonfinite(nv.y) || nonfinite(nv.z) || nonfinite(nv.w);
-        if (lj < g.nyl) {
-            float4 p = *reinterpret_cast<const float4 *>(f.p + rp);
-            p.x = p.x + pc.x;
-            p.y = p.y + pc.y;
-            p.z = p.z + pc.z;
-            p.w = p.w + pc.w;
-            *reinterpret_cast<float4 *>(f.p + rp) = p;
+        for (int lj = l0; lj < l1; ++lj) {
+            const int j = g.j0 + lj;
+            const bool vrow = (j != 0 && j != g.ny);
+            float4 pc = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (lj < g.nyl || vrow) pc = *reinterpret_cast<const float4 *>(pp + (long)lj * nx + i0);
+            cf4_row<SP>(g, f, pp, inlet, dt, i0, lj, pc, vrow ? pb : make_float4(0.f, 0.f, 0.f, 0.f),
+                        du, dv, mu, mv, bad);
+            pb = pc;
         }
     }
     flag_nonfinite(c, bad);
@@ -1302,6 +1372,18 @@ void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hi
     if (vec && g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) &&
         a16(f.v_star)) {
         const int nbx = cdiv(g.nx / 4, kBlock);
+        static const bool march = [] {
+            const char *e = getenv("CFD_CF_MARCH");
+            return !(e && atoi(e) == 0);
+        }();
+        if (march) {
+            const dim3 grid(nbx * cdiv(g.nyl + 1, kCfRows));
+            if (g.sp_pow2)
+                hipLaunchKernelGGL(k_correct_finish4m<1>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+            else
+                hipLaunchKernelGGL(k_correct_finish4m<0>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+            return;
+        }
         const long ntiles = (long)nbx * (g.nyl + 1);
         const int blocks = (int)std::min<long>(ntiles, 8L * g.n_cu);
         if (g.sp_pow2)
