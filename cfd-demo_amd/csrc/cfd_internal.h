@@ -54,6 +54,7 @@ struct Ctl {
     uint32_t nonfinite_step;   // sticky: simulation_step after the first step whose
                                // velocities were not all finite (0 = never)
     uint32_t vis[2];        // render: max key, max ~key of the derived field (cfd_render.hip)
+    uint32_t done;          // workgroups finished (last-workgroup folds); 0 between launches
     uint64_t sweeps_total;
     int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
     uint32_t err[kMaxSweeps];        // per-sweep max |p'new - p'| as f32 bits
@@ -128,7 +129,10 @@ void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipSt
 // both schemes' predictors + divergence in one row march (cfd_predict_march.hip),
 // when predict_march_ok(): replaces launch_predict + the step's first divergence
 bool predict_march_ok(const Geom &g, const Fields &f);
-void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+// set_inlet: also set Ctl::inlet from Ctl::step (k_step_begin's ramp,
+// model.rs:311-316) — the step's k_step_begin is then not launched
+void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
+                          bool set_inlet = false);
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s);
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).
@@ -238,7 +242,12 @@ void launch_mg_final_residual(const MgLevel &L, const float *p, uint32_t *slots,
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s);
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);
-void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
+// fold_finalize: the finish launch also does launch_step_finalize's work
+// (its last workgroup; only where correct_finish_folds_finalize() says the
+// marching form runs, and only with no all-reduce between the two)
+bool correct_finish_folds_finalize(const Geom &g, const Fields &f);
+void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
+                           bool fold_finalize = false);
 void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s);
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 

@@ -907,6 +907,56 @@ __device__ __forceinline__ float cf_u_face(const Geom &g, float inlet, float dt,
 // Same values and maxima as k_correct_finish (one float per thread held the
 // kernel near 4.7 TB/s, like the divergence before it went to float4).
 // Requires 16-byte aligned p', p, v*, v (checked by the launcher).
+// k_step_finalize's work (model.rs:333-377, :877-889) for one workgroup.
+// COHERENT: run by the last workgroup of the launch that published the step
+// maxima (k_correct_finish4m's fold): the maxima and the non-finite flag were
+// written by other workgroups' atomics, so they are read with device-scope
+// atomic loads (from L2, never a stale per-CU cache line).
+template <bool COHERENT>
+__device__ __forceinline__ uint32_t ld_ctl_t(const uint32_t *p) {
+    return COHERENT ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+template <bool COHERENT>
+__device__ __forceinline__ void step_finalize_body(const Geom &g, const Fields &f) {
+    auto ld_ctl = [](const uint32_t *p) { return ld_ctl_t<COHERENT>(p); };
+    Ctl *c = f.ctl;
+    if (threadIdx.x < 4) {   // fold the spread step maxima (sharded: already folded)
+        uint32_t *set = f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride;
+        uint32_t v = ld_ctl(&c->red[threadIdx.x]);
+        for (int s = 0; s < kResSlots; ++s) {
+            v = max(v, ld_ctl(&set[s * kResStride]));
+            set[s * kResStride] = 0u;
+        }
+        c->red[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    // failure detection (SURVEY.md §5): red[4] is this step's non-finite flag
+    // (all-reduced across slabs with the maxima); the first such step sticks
+    if (ld_ctl(&c->red[4]) && !c->nonfinite_step) {
+        c->nonfinite_step = c->step + 1u;
+        if (f.host_nonfinite) *f.host_nonfinite = c->step + 1u;   // zero-copy host mirror
+    }
+    c->res_u = __uint_as_float(c->red[0]);
+    c->res_v = __uint_as_float(c->red[1]);
+    const float max_vel = fmaxf(__uint_as_float(c->red[2]), __uint_as_float(c->red[3]));
+    c->step += 1u;
+    c->time = c->time + c->dt;
+    const float previous_dt = c->dt;
+    float new_dt;
+    if (max_vel == 0.0f) {
+        new_dt = c->dt;
+    } else {
+        const float cfl = 0.2f;
+        const float dt_cfl = cfl * fminf(g.dx, g.dy) / max_vel;
+        new_dt = fminf(dt_cfl, c->dt);
+    }
+    c->dt = (new_dt > previous_dt) ? fminf(new_dt, previous_dt * 1.1f) : new_dt;
+    c->red[0] = c->red[1] = c->red[2] = c->red[3] = c->red[4] = 0u;
+}
+
+__global__ void k_step_finalize(Geom g, Fields f) { step_finalize_body<false>(g, f); }
+
 // One row of k_correct_finish4's work for the 4 columns i0..i0+3 of local
 // row lj: pc = p' row lj, pb = p' row lj-1 (loaded by the caller), the step
 // maxima and the non-finite flag accumulate into du..bad.
@@ -1033,8 +1083,10 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
 // k_correct_finish4 with a thread marching down a band of kCfRows rows of its
 // 4 columns: p' row lj, loaded for row lj, is row lj+1's lower neighbour (the
 // v correction's p'(j-1)), so every p' row crosses HBM once instead of twice.
+// FIN: the launch's last workgroup also does k_step_finalize's work (an
+// unsharded step has no all-reduce between the two): one launch less per step.
 constexpr int kCfRows = 16;
-template <int SP>
+template <int SP, bool FIN>
 __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, float dt_override,
                                                              int nbx) {
     Ctl *c = f.ctl;
@@ -1083,6 +1135,17 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, f
         for (int w = 0; w < kBlock / 64; ++w) r = fmaxf(r, red[w][threadIdx.x]);
         publish_max(f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride, bid, r);
     }
+    if (!FIN) return;
+    // last workgroup to finish: every other one's maxima and flag are out
+    __shared__ unsigned ticket;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) ticket = atomicAdd(&c->done, 1u);
+    __syncthreads();
+    if (ticket != gridDim.x - 1) return;
+    __threadfence();
+    step_finalize_body<true>(g, f);
+    if (threadIdx.x == 0) c->done = 0u;
 }
 
 // ------------------------------------------------- step reductions (K7)
@@ -1124,42 +1187,6 @@ __global__ __launch_bounds__(kBlock) void k_step_reduce(Geom g, Fields f) {
 }
 
 // update() epilogue (model.rs:347-377): residuals, step/time, CFL dt.
-__global__ void k_step_finalize(Geom g, Fields f) {
-    Ctl *c = f.ctl;
-    if (threadIdx.x < 4) {   // fold the spread step maxima (sharded: already folded)
-        uint32_t *set = f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride;
-        uint32_t v = c->red[threadIdx.x];
-        for (int s = 0; s < kResSlots; ++s) {
-            v = max(v, set[s * kResStride]);
-            set[s * kResStride] = 0u;
-        }
-        c->red[threadIdx.x] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    // failure detection (SURVEY.md §5): red[4] is this step's non-finite flag
-    // (all-reduced across slabs with the maxima); the first such step sticks
-    if (c->red[4] && !c->nonfinite_step) {
-        c->nonfinite_step = c->step + 1u;
-        if (f.host_nonfinite) *f.host_nonfinite = c->step + 1u;   // zero-copy host mirror
-    }
-    c->res_u = __uint_as_float(c->red[0]);
-    c->res_v = __uint_as_float(c->red[1]);
-    const float max_vel = fmaxf(__uint_as_float(c->red[2]), __uint_as_float(c->red[3]));
-    c->step += 1u;
-    c->time = c->time + c->dt;
-    const float previous_dt = c->dt;
-    float new_dt;
-    if (max_vel == 0.0f) {
-        new_dt = c->dt;
-    } else {
-        const float cfl = 0.2f;
-        const float dt_cfl = cfl * fminf(g.dx, g.dy) / max_vel;
-        new_dt = fminf(dt_cfl, c->dt);
-    }
-    c->dt = (new_dt > previous_dt) ? fminf(new_dt, previous_dt * 1.1f) : new_dt;
-    c->red[0] = c->red[1] = c->red[2] = c->red[3] = c->red[4] = 0u;
-}
 
 
 inline int copy_grid(size_t n4) {
@@ -1363,7 +1390,19 @@ void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_overrid
                            dt_override, nbx);
 }
 
-void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+bool correct_finish_folds_finalize(const Geom &g, const Fields &f) {
+    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    const char *v = getenv("CFD_CF_VEC"), *m = getenv("CFD_CF_MARCH"), *fz = getenv("CFD_CF_FOLD");
+    // opt-in (CFD_CF_FOLD=1): the device-scope release fence every workgroup
+    // needs before its ticket writes its XCD's L2 back (buffer_wbl2; the 8
+    // XCDs have separate L2s), which cost the step 90 us against the ~8 us
+    // launch it saves (r2: 1.318 vs 1.226 ms per step)
+    return fz && atoi(fz) == 1 && !(v && atoi(v) == 0) && !(m && atoi(m) == 0) &&
+           g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star);
+}
+
+void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
+                           bool fold_finalize) {
     static const int vec = [] {
         const char *e = getenv("CFD_CF_VEC");
         return e ? atoi(e) : 1;
@@ -1378,10 +1417,14 @@ void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hi
         }();
         if (march) {
             const dim3 grid(nbx * cdiv(g.nyl + 1, kCfRows));
-            if (g.sp_pow2)
-                hipLaunchKernelGGL(k_correct_finish4m<1>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+            if (g.sp_pow2 && fold_finalize)
+                hipLaunchKernelGGL((k_correct_finish4m<1, true>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+            else if (g.sp_pow2)
+                hipLaunchKernelGGL((k_correct_finish4m<1, false>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+            else if (fold_finalize)
+                hipLaunchKernelGGL((k_correct_finish4m<0, true>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
             else
-                hipLaunchKernelGGL(k_correct_finish4m<0>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+                hipLaunchKernelGGL((k_correct_finish4m<0, false>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
             return;
         }
         const long ntiles = (long)nbx * (g.nyl + 1);

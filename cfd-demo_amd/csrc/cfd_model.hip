@@ -840,7 +840,7 @@ struct cfd_model {
         const bool march = predict_march_ok(g, f);
         const bool fused = march || predict_div_fused(g, f);
         if (march)
-            launch_predict_march(g, f, dt_override, stream);
+            launch_predict_march(g, f, dt_override, stream, finish && step_begin_folded);
         else if (fused)
             launch_predict_div(g, f, dt_override, stream);
         else
@@ -852,7 +852,7 @@ struct cfd_model {
             first_divergence(host_driven() ? -1 : 0);
             int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
             if (rc) return rc;
-            launch_correct_finish(g, f, dt_override, stream);
+            launch_correct_finish(g, f, dt_override, stream, step_finalize_folded);
             HIP_TRY(hipGetLastError());
             return 0;
         }
@@ -892,10 +892,18 @@ struct cfd_model {
     // rec_step: record the step's GPU time for cfd_get_residuals (the last
     // step of a cfd_update_n batch only: every event record on the stream
     // costs the step a few microseconds of dispatch)
+    bool step_begin_folded = false, step_finalize_folded = false;   // this step's (enqueue_update)
     int enqueue_update(bool rec_step = true) {
         if (rec_step) HIP_TRY(hipEventRecord(ev_step0, stream));
         const bool fused = params.corrector_passes == 0;
-        launch_step_begin(g, f, fused ? 0 : 1, stream);
+        // one launch less each side of the step where the fused kernels can
+        // carry the work: the predictor march sets the inlet ramp (all
+        // k_step_begin does when nothing is copied), and the corrector finish's
+        // last workgroup does k_step_finalize's (unsharded: no all-reduce
+        // between the two)
+        step_begin_folded = fused && predict_march_ok(g, f);
+        step_finalize_folded = fused && !sharded() && correct_finish_folds_finalize(g, f);
+        if (!step_begin_folded) launch_step_begin(g, f, fused ? 0 : 1, stream);
         int rc = exchange_uv();
         if (rc) return rc;
         rc = enqueue_piso(kNaN, fused);
@@ -904,7 +912,7 @@ struct cfd_model {
         if (sharded()) launch_fold_slots(f.ctl->red, f.red_slots, 4, stream);
         rc = allreduce_max_u32(f.ctl->red, 5);   // maxima + the non-finite flag
         if (rc) return rc;
-        launch_step_finalize(g, f, stream);
+        if (!step_finalize_folded) launch_step_finalize(g, f, stream);
         HIP_TRY(hipGetLastError());
         if (rec_step) HIP_TRY(hipEventRecord(ev_step1, stream));
         if (timing) timed_steps++;

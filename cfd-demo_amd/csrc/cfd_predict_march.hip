@@ -227,7 +227,16 @@ struct PredMarch {
 template <int SCHEME, int SP, bool MASK, int R>
 __global__ __launch_bounds__(kBlock, CFD_PM_WPE) void k_predict_march(Geom g, Fields f, float dt_override,
                                                           int glo, int u_hi, int v_hi, int nwc,
-                                                          int nseg) {
+                                                          int nseg, int set_inlet) {
+    if (set_inlet && blockIdx.x == 0 && threadIdx.x == 0) {
+        // k_step_begin's work when it copies nothing: the inlet ramp
+        // (simulation_step as f32 / ramp_up_steps as f32) * target (model.rs:311-316),
+        // read by the corrector finish at the end of the step
+        Ctl *c = f.ctl;
+        const uint32_t st = c->step;
+        c->inlet = st < 100u ? ((float)st / 100.0f) * g.target_inlet : g.target_inlet;
+        c->go[0] = 1;
+    }
     PredMarch<SCHEME, SP, MASK, R> m;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int lane = (int)threadIdx.x & 63;
@@ -283,7 +292,8 @@ bool predict_march_ok(const Geom &g, const Fields &f) {
            (uint64_t)f.v_alloc * 4u < (1ull << 31);
 }
 
-void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
+void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
+                          bool set_inlet) {
     const int glo = (g.j0 > 1 ? g.j0 : 1) - g.j0;
     const int u_hi = ((g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2)) - g.j0;
     const int v_hi = ((g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1)) - g.j0;
@@ -297,7 +307,7 @@ void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hip
     const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
 #define CFD_LAUNCH_PM(SC, SPV, MK, R)                                                              \
     hipLaunchKernelGGL((k_predict_march<SC, SPV, MK, R>), grid, dim3(kBlock), 0, s, g, f, dt_override, \
-                       glo, u_hi, v_hi, nwc, nseg)
+                       glo, u_hi, v_hi, nwc, nseg, set_inlet ? 1 : 0)
 #define CFD_LAUNCH_PM3(SC, SPV, MK) \
     if (rows == 8) CFD_LAUNCH_PM(SC, SPV, MK, 8); else CFD_LAUNCH_PM(SC, SPV, MK, 4)
 #define CFD_LAUNCH_PM2(SC, SPV) \
