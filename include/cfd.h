@@ -73,7 +73,10 @@ enum { CFD_INLET_UNIFORM = 0, CFD_INLET_PARABOLIC = 1 };
  * :775-795 + :1344-1470): p' restarts from 0 each solve, arithmetic in double
  * with f32 storage as in the script; SOR is swept red-black (omega 1.7,
  * jacobi_iters iterations, early exit at p_tol); MULTIGRID runs 3 V-cycles and
- * reports max |A p' - rhs|.  Unsharded models only. */
+ * reports max |A p' - rhs|.  Both run on sharded models too: SOR per slab
+ * with a 2-row p' exchange per iteration (>= 16 interior rows and halo depth
+ * >= 2 per slab), MULTIGRID by gathering the rhs and solving the whole grid on
+ * every rank (bit-identical to the unsharded solve). */
 enum { CFD_SOLVER_JACOBI = 0, CFD_SOLVER_SOR = 1, CFD_SOLVER_MULTIGRID = 2 };
 enum { CFD_BC_CHANNEL = 0, CFD_BC_CAVITY = 1 };
 typedef struct {
