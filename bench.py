@@ -187,6 +187,33 @@ def roofline_entry(model, nx, nyl, launch_ms, bench_kernel_note=None):
     }
 
 
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 4   # wave64 VALU instructions/s: 256 CUs x 4 SIMDs, one per 4 cycles at 2.4 GHz
+
+
+def roofline_valu(kernel, slab, launch_ms):
+    """The Jacobi launch's binding resource on a MALL-resident slab is VALU
+    issue: SQ_INSTS_VALU per launch from the newest committed
+    PMC pass on this slab (tools/pmc_valu.py) over the measured launch time,
+    against the chip's wave64 VALU issue rate at the 2.4 GHz max clock."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_valu*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and d.get("workload") == slab and k.get("SQ_INSTS_VALU") and launch_ms > 0:
+            rate = k["SQ_INSTS_VALU"] / (launch_ms * 1e-3)
+            return {"bound": "valu", "achieved": rate / 1e9, "peak": VALU_ISSUE_PEAK / 1e9,
+                    "unit": "G wave64-VALU-instructions/s", "frac": rate / VALU_ISSUE_PEAK,
+                    "valu_insts_per_launch": k["SQ_INSTS_VALU"],
+                    "source": os.path.relpath(path, ROOT),
+                    "note": "SQ_INSTS_VALU (PMC, same kernel and slab) / launch time; peak = 1024 "
+                            "SIMDs x 1 wave64 instruction per 4 cycles x 2.4 GHz (the chip holds "
+                            "a lower clock under load, so frac is conservative)"}
+    return None
+
+
 def pmc_traffic(kernel, slab):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*/pmc_traffic.json, tools/pmc_traffic.py: 2 x FETCH_SIZE +
@@ -323,6 +350,7 @@ def main():
     launches = max(args.steps * model.launches_per_solve(), 1)
     launch_ms = tm["solve_ms"] / launches
     roof = roofline_entry(model, nx, model.nyl, launch_ms)
+    roof_valu = roofline_valu(kern["name"], f"{nx}x{model.nyl}", launch_ms)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -353,6 +381,7 @@ def main():
                              "FMA-corrected (proven exact, 2^32 inputs)"][kcfg["fastdiv"]],
             },
             "roofline": roof,
+            "roofline_valu": roof_valu,
             "solve_fraction_of_step": tm["solve_ms"] / tm["step_ms"] if tm["step_ms"] else None,
             # a timed-mode step moves 2,498 B per pressure cell
             # when every pass streams its fields (P = 1 solve, K = 200 sweeps);

@@ -37,6 +37,8 @@ if [ "${PMC:-0}" = 1 ]; then
   export TMPDIR=/tmp
   step pmc_fetch 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_$TAG -o fetch --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2
   step pmc_write 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_$TAG -o write --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2
+  step pmc_valu 300 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/pmc_$TAG -o valu --output-format csv -- python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2
+  python tools/pmc_valu.py gpurun_out/pmc_$TAG/valu_counter_collection.csv --workload 4096x4096 --command "python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2" -o gpurun_out/pmc_$TAG/pmc_valu.json
   python tools/pmc_traffic.py gpurun_out/pmc_$TAG/fetch_counter_collection.csv gpurun_out/pmc_$TAG/write_counter_collection.csv --workload 4096x4096 --command "python bench.py --no-cpu-baseline --no-parity --no-control --develop 30 --warmup 0 --steps 2" -o gpurun_out/pmc_$TAG/pmc_traffic.json
 fi
 echo DONE
