@@ -246,8 +246,17 @@ void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);
 // (its last workgroup; only where correct_finish_folds_finalize() says the
 // marching form runs, and only with no all-reduce between the two)
 bool correct_finish_folds_finalize(const Geom &g, const Fields &f);
+// A fixed-count solve's deferred k_finalize_solve (sf != null): the finish
+// launch's workgroup 0 does it (marching form; otherwise the finalize is
+// launched first), every workgroup reading p' from pp_new, the buffer the
+// flip makes current.  correct_finish_march(): the marching form runs.
+struct SolveFinalizeArgs {
+    const float *pp_new;
+    int pass, iters, check_break, flips;
+};
+bool correct_finish_march(const Geom &g, const Fields &f);
 void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
-                           bool fold_finalize = false);
+                           bool fold_finalize = false, const SolveFinalizeArgs *sf = nullptr);
 void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s);
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 

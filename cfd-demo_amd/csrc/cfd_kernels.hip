@@ -633,9 +633,12 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
 // End of a pressure solve: how many sweeps ran, which buffer is current, the
 // returned residual (model.rs:816-823), and whether the corrector loop goes on
 // (model.rs:721-723).  Resets the per-sweep slots for the next solve.
-__global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
-                                                           int check_break, int flips,
-                                                           int exact_flips) {
+// k_finalize_solve's work (one workgroup of kBlock threads): fold the solve's
+// residual slots into Ctl::err, count the sweeps that ran, flip the current
+// p' buffer, set the next corrector pass's go flag, clear err[].
+__device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields &f, int pass,
+                                                    int iters, int check_break, int flips,
+                                                    int exact_flips) {
     Ctl *c = f.ctl;
     __shared__ int go_s;
     // fold the spread residual slots into err[]: every sweep's with the
@@ -673,6 +676,12 @@ __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int
     __syncthreads();
     if (go_s)
         for (int k = threadIdx.x; k < iters; k += blockDim.x) c->err[k] = 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
+                                                           int check_break, int flips,
+                                                           int exact_flips) {
+    solve_finalize_body(g, f, pass, iters, check_break, flips, exact_flips);
 }
 
 // dst[q] = max(dst[q], slots of set q), then zero the slots (q < n).
@@ -1086,10 +1095,19 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, fl
 // FIN: the launch's last workgroup also does k_step_finalize's work (an
 // unsharded step has no all-reduce between the two): one launch less per step.
 constexpr int kCfRows = 16;
-template <int SP, bool FIN>
+// FS: workgroup 0 first does the solve's k_finalize_solve work (fixed-count
+// solve: the flip count is the host's), so that launch goes; every workgroup
+// takes p' from pp_new (the buffer the flip makes current) instead of
+// reading Ctl::cur, which workgroup 0 rewrites.
+struct FinDefer {
+    const float *pp_new;
+    int pass, iters, check_break, flips;
+};
+template <int SP, bool FIN, bool FS>
 __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, float dt_override,
-                                                             int nbx) {
+                                                             int nbx, FinDefer fd) {
     Ctl *c = f.ctl;
+    if (FS && blockIdx.x == 0) solve_finalize_body(g, f, fd.pass, fd.iters, fd.check_break, fd.flips, 0);
     const int nx = g.nx;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
     bool bad = false;
@@ -1098,7 +1116,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, f
     const int l0 = (bid / nbx) * kCfRows, l1 = min(l0 + kCfRows, g.nyl + 1);
     const float dt = dt_of(c, dt_override);
     const float inlet = c->inlet;
-    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+    const float *__restrict__ pp = FS ? fd.pp_new : (c->cur ? f.pp[1] : f.pp[0]);
     if (i0 < nx) {
         float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
         {
@@ -1401,8 +1419,15 @@ bool correct_finish_folds_finalize(const Geom &g, const Fields &f) {
            g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star);
 }
 
+bool correct_finish_march(const Geom &g, const Fields &f) {
+    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    const char *v = getenv("CFD_CF_VEC"), *m = getenv("CFD_CF_MARCH");
+    return !(v && atoi(v) == 0) && !(m && atoi(m) == 0) && g.nx % 4 == 0 && a16(f.pp[0]) &&
+           a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star);
+}
+
 void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
-                           bool fold_finalize) {
+                           bool fold_finalize, const SolveFinalizeArgs *sf) {
     static const int vec = [] {
         const char *e = getenv("CFD_CF_VEC");
         return e ? atoi(e) : 1;
@@ -1417,16 +1442,27 @@ void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hi
         }();
         if (march) {
             const dim3 grid(nbx * cdiv(g.nyl + 1, kCfRows));
-            if (g.sp_pow2 && fold_finalize)
-                hipLaunchKernelGGL((k_correct_finish4m<1, true>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
-            else if (g.sp_pow2)
-                hipLaunchKernelGGL((k_correct_finish4m<1, false>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
-            else if (fold_finalize)
-                hipLaunchKernelGGL((k_correct_finish4m<0, true>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
-            else
-                hipLaunchKernelGGL((k_correct_finish4m<0, false>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+            FinDefer fd{};
+            if (sf) fd = FinDefer{sf->pp_new, sf->pass, sf->iters, sf->check_break, sf->flips};
+#define CFD_LAUNCH_CF4M(SPV, FINV, FSV)                                                          \
+            hipLaunchKernelGGL((k_correct_finish4m<SPV, FINV, FSV>), grid, dim3(kBlock), 0, s, g, f, \
+                               dt_override, nbx, fd)
+#define CFD_LAUNCH_CF4M2(SPV, FINV) \
+            if (sf) { CFD_LAUNCH_CF4M(SPV, FINV, true); } else { CFD_LAUNCH_CF4M(SPV, FINV, false); }
+            if (g.sp_pow2 && fold_finalize) {
+                CFD_LAUNCH_CF4M2(1, true);
+            } else if (g.sp_pow2) {
+                CFD_LAUNCH_CF4M2(1, false);
+            } else if (fold_finalize) {
+                CFD_LAUNCH_CF4M2(0, true);
+            } else {
+                CFD_LAUNCH_CF4M2(0, false);
+            }
+#undef CFD_LAUNCH_CF4M2
+#undef CFD_LAUNCH_CF4M
             return;
         }
+        if (sf) launch_finalize_solve(g, f, sf->pass, sf->iters, sf->check_break, sf->flips, s);
         const long ntiles = (long)nbx * (g.nyl + 1);
         const int blocks = (int)std::min<long>(ntiles, 8L * g.n_cu);
         if (g.sp_pow2)

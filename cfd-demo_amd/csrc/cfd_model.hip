@@ -738,7 +738,14 @@ struct cfd_model {
             if (rc) return rc;
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
         }
-        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream);
+        if (defer_finalize) {
+            // the corrector finish's workgroup 0 does it (one launch less)
+            fin_deferred = SolveFinalizeArgs{f.pp[(host_cur + launches) & 1], pass, iters,
+                                             pass >= 1 ? 1 : 0, launches};
+            fin_pending = true;
+        } else {
+            launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream);
+        }
         HIP_TRY(hipGetLastError());
         if (evt) {
             solve_events.emplace_back(e0, e1);
@@ -850,9 +857,18 @@ struct cfd_model {
         };
         if (finish) {
             first_divergence(host_driven() ? -1 : 0);
+            // a fixed-count Jacobi solve (its flip count is the host's) hands
+            // its finalize to the corrector finish's first workgroup
+            defer_finalize = !host_driven() && !g.tol_enabled &&
+                             params.pressure_solver == CFD_SOLVER_JACOBI && correct_finish_march(g, f) &&
+                             defer_finalize_env;
+            fin_pending = false;
             int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
+            defer_finalize = false;
             if (rc) return rc;
-            launch_correct_finish(g, f, dt_override, stream, step_finalize_folded);
+            launch_correct_finish(g, f, dt_override, stream, step_finalize_folded,
+                                  fin_pending ? &fin_deferred : nullptr);
+            fin_pending = false;
             HIP_TRY(hipGetLastError());
             return 0;
         }
@@ -893,6 +909,16 @@ struct cfd_model {
     // step of a cfd_update_n batch only: every event record on the stream
     // costs the step a few microseconds of dispatch)
     bool step_begin_folded = false, step_finalize_folded = false;   // this step's (enqueue_update)
+    // the step's solve finalize handed to the corrector finish (enqueue_piso)
+    bool defer_finalize = false, fin_pending = false;
+    SolveFinalizeArgs fin_deferred{};
+    // opt-in (CFD_SOLVE_FIN_FOLD=1): one launch less, but workgroup 0's extra
+    // serial work lengthens the finish by as much (r2: 1.2347/1.2298 vs
+    // 1.2342/1.2358 ms per step, tools/fin_ab.sh)
+    bool defer_finalize_env = [] {
+        const char *e = getenv("CFD_SOLVE_FIN_FOLD");
+        return e && atoi(e) == 1;
+    }();
     int enqueue_update(bool rec_step = true) {
         if (rec_step) HIP_TRY(hipEventRecord(ev_step0, stream));
         const bool fused = params.corrector_passes == 0;
