@@ -180,11 +180,18 @@ struct cfd_model {
         if (!st) st = stream;
         if (hub) return exchange_local(id, kind, depth, st);
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        RCCL_TRY(ncclGroupStart());
+        int rc = exchange_ops(id, kind, depth, st);
+        RCCL_TRY(ncclGroupEnd());
+        return rc;
+    }
+
+    // The sends and receives of one field's ghost exchange (inside a group).
+    int exchange_ops(int id, int kind, int depth, hipStream_t st) {
         float *base = field_ptr(id);
         const size_t pitch = field_pitch(id);
         int h[6];
         plan_halo(kind, g.nyl, depth, rank, n_ranks, h);
-        RCCL_TRY(ncclGroupStart());
         if (h[2] > 0) {
             RCCL_TRY(ncclSend(base + (long)h[0] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
                               rank - 1, comm, st));
@@ -197,7 +204,6 @@ struct cfd_model {
             RCCL_TRY(ncclRecv(base + (long)h[4] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
                               rank + 1, comm, st));
         }
-        RCCL_TRY(ncclGroupEnd());
         return 0;
     }
 
@@ -225,11 +231,21 @@ struct cfd_model {
         return 0;
     }
 
-    // u/v ghost rows before the predictors.
+    // u/v ghost rows before the predictors: both fields in
+    // ONE RCCL group (one launch latency over xGMI instead of two).
     int exchange_uv() {
-        int rc = exchange(FLD_U, HALO_U, 2);
-        if (rc) return rc;
-        return exchange(FLD_V, HALO_V, 2);
+        if (!sharded()) return 0;
+        if (hub) {
+            int rc = exchange_local(FLD_U, HALO_U, 2, stream);
+            if (rc) return rc;
+            return exchange_local(FLD_V, HALO_V, 2, stream);
+        }
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        RCCL_TRY(ncclGroupStart());
+        int rc = exchange_ops(FLD_U, HALO_U, 2, stream);
+        if (!rc) rc = exchange_ops(FLD_V, HALO_V, 2, stream);
+        RCCL_TRY(ncclGroupEnd());
+        return rc;
     }
 
     // p' halo: `rows` owned boundary rows of buffer `buf` each way.
