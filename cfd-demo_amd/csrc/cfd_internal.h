@@ -49,7 +49,8 @@ struct Ctl {
     uint32_t n_exec_last;   // sweeps executed by the last solve
     float last_p;           // last_pressure_residual
     float res_u, res_v;     // last_u_residual / last_v_residual
-    uint32_t red[5];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|; red[4]:
+    uint32_t red[6];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|; red[5]: the last
+                            // solve's residual (all-reduced with the maxima on slabs); red[4]:
                             // non-finite flag (1: some new u/v value is NaN or +-Inf)
     uint32_t nonfinite_step;   // sticky: simulation_step after the first step whose
                                // velocities were not all finite (0 = never)

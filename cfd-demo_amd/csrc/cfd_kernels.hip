@@ -666,6 +666,7 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
             // `flips` (host-known launch count) for fixed-count solves
             c->cur = (c->cur + ((g.tol_enabled && !exact_flips) ? n : flips)) & 1;
             c->last_p = res;
+            c->red[5] = __float_as_uint(res);   // the step-end all-reduce carries it (slabs)
             c->n_exec_last = (uint32_t)n;
             c->sweeps_total += (uint64_t)n;
         }
@@ -961,7 +962,10 @@ __device__ __forceinline__ void step_finalize_body(const Geom &g, const Fields &
         new_dt = fminf(dt_cfl, c->dt);
     }
     c->dt = (new_dt > previous_dt) ? fminf(new_dt, previous_dt * 1.1f) : new_dt;
-    c->red[0] = c->red[1] = c->red[2] = c->red[3] = c->red[4] = 0u;
+    // the step's last solve residual: all-reduced across slabs with the
+    // maxima (a sharded fixed-count step skips the solve's own all-reduce)
+    c->last_p = __uint_as_float(ld_ctl(&c->red[5]));
+    c->red[0] = c->red[1] = c->red[2] = c->red[3] = c->red[4] = c->red[5] = 0u;
 }
 
 __global__ void k_step_finalize(Geom g, Fields f) { step_finalize_body<false>(g, f); }

@@ -748,10 +748,12 @@ struct cfd_model {
                 }
             }
             const int last = iters > 0 ? iters - 1 : 0;
-            launch_fold_slots(f.ctl->err + last, f.err_slots + (size_t)last * kResSlots * kResStride,
-                              1, stream);
-            int rc = allreduce_max_u32(f.ctl->err + last, 1);
-            if (rc) return rc;
+            if (!merge_res_allreduce) {
+                launch_fold_slots(f.ctl->err + last,
+                                  f.err_slots + (size_t)last * kResSlots * kResStride, 1, stream);
+                int rc = allreduce_max_u32(f.ctl->err + last, 1);
+                if (rc) return rc;
+            }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
         }
         if (defer_finalize) {
@@ -879,7 +881,12 @@ struct cfd_model {
                              params.pressure_solver == CFD_SOLVER_JACOBI && correct_finish_march(g, f) &&
                              defer_finalize_env;
             fin_pending = false;
+            // a fixed-count step on slabs needs the solve's residual only for
+            // reporting: it rides the step-end all-reduce (Ctl::red[5]) instead
+            // of an all-reduce of its own
+            merge_res_allreduce = sharded() && !host_driven();
             int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
+            merge_res_allreduce = false;
             defer_finalize = false;
             if (rc) return rc;
             launch_correct_finish(g, f, dt_override, stream, step_finalize_folded,
@@ -926,7 +933,7 @@ struct cfd_model {
     // costs the step a few microseconds of dispatch)
     bool step_begin_folded = false, step_finalize_folded = false;   // this step's (enqueue_update)
     // the step's solve finalize handed to the corrector finish (enqueue_piso)
-    bool defer_finalize = false, fin_pending = false;
+    bool defer_finalize = false, fin_pending = false, merge_res_allreduce = false;
     SolveFinalizeArgs fin_deferred{};
     // opt-in (CFD_SOLVE_FIN_FOLD=1): one launch less, but workgroup 0's extra
     // serial work lengthens the finish by as much (r2: 1.2347/1.2298 vs
@@ -952,7 +959,7 @@ struct cfd_model {
         if (rc) return rc;
         if (!fused) launch_step_reduce(g, f, stream);
         if (sharded()) launch_fold_slots(f.ctl->red, f.red_slots, 4, stream);
-        rc = allreduce_max_u32(f.ctl->red, 5);   // maxima + the non-finite flag
+        rc = allreduce_max_u32(f.ctl->red, 6);   // maxima, non-finite flag, solve residual
         if (rc) return rc;
         if (!step_finalize_folded) launch_step_finalize(g, f, stream);
         HIP_TRY(hipGetLastError());
