@@ -92,7 +92,7 @@ struct cfd_model {
     // sharded fixed-count solves: the boundary bands and their p' exchange run
     // on cstream while the interior runs on stream (SURVEY.md §8(e) overlap)
     hipStream_t cstream = nullptr;
-    hipEvent_t ev_ov0 = nullptr, ev_ov1 = nullptr;
+    hipEvent_t ev_ov0 = nullptr, ev_ov1 = nullptr, ev_rhs = nullptr;
     bool overlap = true;   // CFD_OVERLAP=0 serialises them
     cfd_grid grid{};
     cfd_params params{};
@@ -705,9 +705,25 @@ struct cfd_model {
             }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
         } else {
-            // the deep-halo sweeps recompute ghost rows, which read rhs there
-            int rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
-            if (rc0) return rc0;
+            // the deep-halo sweeps recompute ghost rows, which read rhs there.
+            // Overlapped (r2): the rhs exchange runs on cstream while the first
+            // launch's interior rows, whose T sweeps read no rhs ghost row
+            // (stage 1 of output rows [a, b) reads rhs rows [a-T+1, b+T-1)),
+            // run on stream; the edge rows follow once the ghosts are in.
+            const bool rhs_ovl = overlap && tmax > 1 && !pp_ghosts_shallow;
+            bool rhs_pending = false;
+            int rc0;
+            if (rhs_ovl) {
+                HIP_TRY(hipEventRecord(ev_ov0, stream));   // rhs written
+                HIP_TRY(hipStreamWaitEvent(cstream, ev_ov0, 0));
+                rc0 = exchange(FLD_RHS, HALO_PP, g.hg, cstream);
+                if (rc0) return rc0;
+                HIP_TRY(hipEventRecord(ev_rhs, cstream));
+                rhs_pending = true;
+            } else {
+                rc0 = exchange(FLD_RHS, HALO_PP, g.hg);
+                if (rc0) return rc0;
+            }
             if (pp_ghosts_shallow) {   // sweep 0 reads p' ghosts hg rows deep
                 rc0 = exchange_pp(host_cur, g.hg);
                 if (rc0) return rc0;
@@ -717,6 +733,20 @@ struct cfd_model {
                 int T, lo, hi, exch;
                 plan_block(g.j0, g.nyl, g.ny, g.hg, it, tmax, iters, &T, &lo, &hi, &exch);
                 const int res = it + T == iters;
+                if (rhs_pending) {
+                    rhs_pending = false;
+                    const int a = std::max(lo, T - 1), b = std::min(hi, g.nyl - T + 1);
+                    const bool split = a < b && !exch;
+                    if (split) launch_jacobi_block(g, f, pass, it, launches, T, a, b, res, stream);
+                    HIP_TRY(hipStreamWaitEvent(stream, ev_rhs, 0));
+                    if (split) {
+                        if (lo < a) launch_jacobi_block(g, f, pass, it, launches, T, lo, a, res, stream);
+                        if (b < hi) launch_jacobi_block(g, f, pass, it, launches, T, b, hi, res, stream);
+                        it += T;
+                        ++launches;
+                        continue;
+                    }
+                }
                 // Overlap: the block before an exchange first
                 // computes the hg-row bands the exchange sends, on cstream, which
                 // then runs the exchange, while the interior rows run on stream.
@@ -1065,6 +1095,7 @@ struct cfd_model {
         if (cstream) (void)hipStreamDestroy(cstream);
         if (ev_ov0) (void)hipEventDestroy(ev_ov0);
         if (ev_ov1) (void)hipEventDestroy(ev_ov1);
+        if (ev_rhs) (void)hipEventDestroy(ev_rhs);
     }
 };
 
@@ -1163,6 +1194,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     HIP_TRY(hipStreamCreateWithFlags(&m->cstream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&m->ev_ov0, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&m->ev_ov1, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&m->ev_rhs, hipEventDisableTiming));
     if (const char *ov = getenv("CFD_OVERLAP")) m->overlap = atoi(ov) != 0;
     HIP_TRY(hipEventCreate(&m->ev_step0));
     HIP_TRY(hipEventCreate(&m->ev_step1));
