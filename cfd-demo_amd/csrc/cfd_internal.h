@@ -132,8 +132,11 @@ void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipSt
 bool predict_march_ok(const Geom &g, const Fields &f);
 // set_inlet: also set Ctl::inlet from Ctl::step (k_step_begin's ramp,
 // model.rs:311-316) — the step's k_step_begin is then not launched
+// [row_lo, row_hi): the divergence rows the launch forms (>= 4 rows; default
+// all owned rows) — a sharded step runs rows [2, nyl-2), which read no u/v
+// ghost row, while the ghost exchange is in flight
 void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
-                          bool set_inlet = false);
+                          bool set_inlet = false, int row_lo = 0, int row_hi = -1);
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,
                        hipStream_t s);
 // One Jacobi sweep over local rows [row_lo, row_hi) (may reach into ghosts).

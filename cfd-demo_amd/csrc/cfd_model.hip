@@ -92,7 +92,7 @@ struct cfd_model {
     // sharded fixed-count solves: the boundary bands and their p' exchange run
     // on cstream while the interior runs on stream (SURVEY.md §8(e) overlap)
     hipStream_t cstream = nullptr;
-    hipEvent_t ev_ov0 = nullptr, ev_ov1 = nullptr, ev_rhs = nullptr;
+    hipEvent_t ev_ov0 = nullptr, ev_ov1 = nullptr, ev_rhs = nullptr, ev_uv = nullptr;
     bool overlap = true;   // CFD_OVERLAP=0 serialises them
     cfd_grid grid{};
     cfd_params params{};
@@ -233,17 +233,18 @@ struct cfd_model {
 
     // u/v ghost rows before the predictors: both fields in
     // ONE RCCL group (one launch latency over xGMI instead of two).
-    int exchange_uv() {
+    int exchange_uv(hipStream_t st = nullptr) {
         if (!sharded()) return 0;
+        if (!st) st = stream;
         if (hub) {
-            int rc = exchange_local(FLD_U, HALO_U, 2, stream);
+            int rc = exchange_local(FLD_U, HALO_U, 2, st);
             if (rc) return rc;
-            return exchange_local(FLD_V, HALO_V, 2, stream);
+            return exchange_local(FLD_V, HALO_V, 2, st);
         }
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
         RCCL_TRY(ncclGroupStart());
-        int rc = exchange_ops(FLD_U, HALO_U, 2, stream);
-        if (!rc) rc = exchange_ops(FLD_V, HALO_V, 2, stream);
+        int rc = exchange_ops(FLD_U, HALO_U, 2, st);
+        if (!rc) rc = exchange_ops(FLD_V, HALO_V, 2, st);
         RCCL_TRY(ncclGroupEnd());
         return rc;
     }
@@ -894,7 +895,15 @@ struct cfd_model {
         // K1-K3: the fused march when it applies, else predictors + divergence
         const bool march = predict_march_ok(g, f);
         const bool fused = march || predict_div_fused(g, f);
-        if (march)
+        if (march && finish && uv_async) {
+            // rows [2, nyl-2) read u rows >= 0 and <= nyl-1 and v rows <= nyl;
+            // the edge rows (4-row launches overlapping the interior ones:
+            // identical values) follow the ghost exchange
+            launch_predict_march(g, f, dt_override, stream, true, 2, g.nyl - 2);
+            HIP_TRY(hipStreamWaitEvent(stream, ev_uv, 0));
+            launch_predict_march(g, f, dt_override, stream, false, 0, 4);
+            launch_predict_march(g, f, dt_override, stream, false, g.nyl - 4, g.nyl);
+        } else if (march)
             launch_predict_march(g, f, dt_override, stream, finish && step_begin_folded);
         else if (fused)
             launch_predict_div(g, f, dt_override, stream);
@@ -964,6 +973,7 @@ struct cfd_model {
     bool step_begin_folded = false, step_finalize_folded = false;   // this step's (enqueue_update)
     // the step's solve finalize handed to the corrector finish (enqueue_piso)
     bool defer_finalize = false, fin_pending = false, merge_res_allreduce = false;
+    bool uv_async = false;   // this step's u/v exchange runs on cstream (enqueue_update)
     SolveFinalizeArgs fin_deferred{};
     // opt-in (CFD_SOLVE_FIN_FOLD=1): one launch less, but workgroup 0's extra
     // serial work lengthens the finish by as much (r2: 1.2347/1.2298 vs
@@ -983,7 +993,19 @@ struct cfd_model {
         step_begin_folded = fused && predict_march_ok(g, f);
         step_finalize_folded = fused && !sharded() && correct_finish_folds_finalize(g, f);
         if (!step_begin_folded) launch_step_begin(g, f, fused ? 0 : 1, stream);
-        int rc = exchange_uv();
+        // slabs: the u/v ghost exchange runs on cstream while the predictor
+        // march forms the rows that read no ghost (enqueue_piso)
+        uv_async = sharded() && overlap && fused && step_begin_folded && g.nyl >= 8;
+        int rc;
+        if (uv_async) {
+            HIP_TRY(hipEventRecord(ev_ov0, stream));   // u, v final (last step's finish)
+            HIP_TRY(hipStreamWaitEvent(cstream, ev_ov0, 0));
+            rc = exchange_uv(cstream);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(ev_uv, cstream));
+        } else {
+            rc = exchange_uv();
+        }
         if (rc) return rc;
         rc = enqueue_piso(kNaN, fused);
         if (rc) return rc;
@@ -1096,6 +1118,7 @@ struct cfd_model {
         if (ev_ov0) (void)hipEventDestroy(ev_ov0);
         if (ev_ov1) (void)hipEventDestroy(ev_ov1);
         if (ev_rhs) (void)hipEventDestroy(ev_rhs);
+        if (ev_uv) (void)hipEventDestroy(ev_uv);
     }
 };
 
@@ -1195,6 +1218,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     HIP_TRY(hipEventCreateWithFlags(&m->ev_ov0, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&m->ev_ov1, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&m->ev_rhs, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&m->ev_uv, hipEventDisableTiming));
     if (const char *ov = getenv("CFD_OVERLAP")) m->overlap = atoi(ov) != 0;
     HIP_TRY(hipEventCreate(&m->ev_step0));
     HIP_TRY(hipEventCreate(&m->ev_step1));

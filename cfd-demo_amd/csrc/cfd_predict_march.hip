@@ -227,7 +227,8 @@ struct PredMarch {
 template <int SCHEME, int SP, bool MASK, int R>
 __global__ __launch_bounds__(kBlock, CFD_PM_WPE) void k_predict_march(Geom g, Fields f, float dt_override,
                                                           int glo, int u_hi, int v_hi, int nwc,
-                                                          int nseg, int set_inlet) {
+                                                          int nseg, int set_inlet, int row_lo,
+                                                          int row_hi) {
     if (set_inlet && blockIdx.x == 0 && threadIdx.x == 0) {
         // k_step_begin's work when it copies nothing: the inlet ramp
         // (simulation_step as f32 / ramp_up_steps as f32) * target (model.rs:311-316),
@@ -244,11 +245,11 @@ __global__ __launch_bounds__(kBlock, CFD_PM_WPE) void k_predict_march(Geom g, Fi
     const int wc = bid % nwc;
     const int seg = (bid / nwc) * (kBlock / 64) + wave;
     if (seg >= nseg) return;   // wave-uniform
-    const int nyl = g.nyl, nx = g.nx;
-    // R rows per segment; the last one ends at nyl and overlaps its
-    // neighbour (both store the same values; no segment reads what another
-    // stores)
-    m.r0 = min(seg * R, nyl - R);
+    const int nx = g.nx;
+    // R rows per segment of the launch's rows [row_lo, row_hi); the last one
+    // ends at row_hi and overlaps its neighbour (both store the same values;
+    // no segment reads what another stores)
+    m.r0 = row_lo + min(seg * R, row_hi - row_lo - R);
     m.r1 = m.r0 + R;
     m.g = &g;
     m.f = f;
@@ -293,7 +294,8 @@ bool predict_march_ok(const Geom &g, const Fields &f) {
 }
 
 void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
-                          bool set_inlet) {
+                          bool set_inlet, int row_lo, int row_hi) {
+    if (row_hi < 0) row_hi = g.nyl;
     const int glo = (g.j0 > 1 ? g.j0 : 1) - g.j0;
     const int u_hi = ((g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2)) - g.j0;
     const int v_hi = ((g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1)) - g.j0;
@@ -301,13 +303,13 @@ void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hip
     // 17 wave columns; 16-row segments measured equal for the first-order
     // scheme and 17 % slower for the second-order one, whose unrolled march
     // then outgrows the instruction cache), 4 on slabs under 8 rows
-    const int rows = g.nyl >= 8 ? 8 : 4;
+    const int rows = row_hi - row_lo >= 8 ? 8 : 4;
     const int nwc = cdiv(g.nx / 4 + 1, 62);
-    const int nseg = cdiv(g.nyl, rows);
+    const int nseg = cdiv(row_hi - row_lo, rows);
     const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
 #define CFD_LAUNCH_PM(SC, SPV, MK, R)                                                              \
     hipLaunchKernelGGL((k_predict_march<SC, SPV, MK, R>), grid, dim3(kBlock), 0, s, g, f, dt_override, \
-                       glo, u_hi, v_hi, nwc, nseg, set_inlet ? 1 : 0)
+                       glo, u_hi, v_hi, nwc, nseg, set_inlet ? 1 : 0, row_lo, row_hi)
 #define CFD_LAUNCH_PM3(SC, SPV, MK) \
     if (rows == 8) CFD_LAUNCH_PM(SC, SPV, MK, 8); else CFD_LAUNCH_PM(SC, SPV, MK, 4)
 #define CFD_LAUNCH_PM2(SC, SPV) \
