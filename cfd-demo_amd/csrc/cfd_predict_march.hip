@@ -38,6 +38,9 @@ namespace {
 #ifndef CFD_PM_WPE
 #define CFD_PM_WPE 3  // minimum waves per SIMD (caps VGPRs at 168)
 #endif
+#ifndef CFD_PM_ROWS_FO
+#define CFD_PM_ROWS_FO 8   // first-order march segment rows (r2: 8 rows 75.0 us, 16 rows 80.4 us)
+#endif
 #ifndef CFD_PM_PD
 #define CFD_PM_PD 1   // prefetch distance (steps) of the u / v rows (1: 88.6 vs 90.3 us SO, r2 pm)
 #endif
@@ -303,15 +306,20 @@ void launch_predict_march(const Geom &g, const Fields &f, float dt_override, hip
     // 17 wave columns; 16-row segments measured equal for the first-order
     // scheme and 17 % slower for the second-order one, whose unrolled march
     // then outgrows the instruction cache), 4 on slabs under 8 rows
-    const int rows = row_hi - row_lo >= 8 ? 8 : 4;
+    // first order: CFD_PM_ROWS_FO rows per segment (compile-time knob, 8)
+    const int big = g.scheme == 0 ? CFD_PM_ROWS_FO : 8;
+    const int span = row_hi - row_lo;
+    const int rows = span >= big ? big : (span >= 8 ? 8 : 4);
     const int nwc = cdiv(g.nx / 4 + 1, 62);
     const int nseg = cdiv(row_hi - row_lo, rows);
     const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
 #define CFD_LAUNCH_PM(SC, SPV, MK, R)                                                              \
     hipLaunchKernelGGL((k_predict_march<SC, SPV, MK, R>), grid, dim3(kBlock), 0, s, g, f, dt_override, \
                        glo, u_hi, v_hi, nwc, nseg, set_inlet ? 1 : 0, row_lo, row_hi)
-#define CFD_LAUNCH_PM3(SC, SPV, MK) \
-    if (rows == 8) CFD_LAUNCH_PM(SC, SPV, MK, 8); else CFD_LAUNCH_PM(SC, SPV, MK, 4)
+#define CFD_LAUNCH_PM3(SC, SPV, MK)                                         \
+    if (CFD_PM_ROWS_FO != 8 && SC == 0 && rows == CFD_PM_ROWS_FO)           \
+        CFD_LAUNCH_PM(SC, SPV, MK, (SC == 0 ? CFD_PM_ROWS_FO : 8));          \
+    else if (rows == 8) CFD_LAUNCH_PM(SC, SPV, MK, 8); else CFD_LAUNCH_PM(SC, SPV, MK, 4)
 #define CFD_LAUNCH_PM2(SC, SPV) \
     if (f.any_pmask) { CFD_LAUNCH_PM3(SC, SPV, true); } else { CFD_LAUNCH_PM3(SC, SPV, false); }
     if (g.scheme == 0) {
