@@ -276,6 +276,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("CFD_BENCH_LOOPBACK") == "1" and world > 1:
+        # rehearsal of the N-GPU run on a one-GPU box (tools/rccl_loopback.py's
+        # trick): every rank on device 0, each its own RCCL "host" so RCCL
+        # connects them through its socket transport; set before RCCL loads
+        os.environ["NCCL_HOSTID"] = f"cfd-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        os.environ.setdefault("NCCL_NET", "Socket")
+        local = 0
     n = max(world, 1)
     if args.gpus != n and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
