@@ -38,6 +38,9 @@ namespace {
 #ifndef CFD_PM_WPE
 #define CFD_PM_WPE 3  // minimum waves per SIMD (caps VGPRs at 168)
 #endif
+#ifndef CFD_PM_USTORE
+#define CFD_PM_USTORE 0    // u* store: 0 one dword-aligned dwordx4 (75.1 us), 1 four dwords (75.7 us)
+#endif
 #ifndef CFD_PM_ROWS_FO
 #define CFD_PM_ROWS_FO 8   // first-order march segment rows (r2: 8 rows 75.0 us, 16 rows 80.4 us)
 #endif
@@ -183,7 +186,16 @@ struct PredMarch {
             const float east = from_right(us[0]);
             if (st_lane) {
                 if (c < nch) {
-                    if (upred) *reinterpret_cast<f4u *>(f.u_star + ku) = (f4u){us[0], us[1], us[2], us[3]};
+                    if (upred) {
+                        if (CFD_PM_USTORE == 0) {   // one dword-aligned 16-byte store
+                            *reinterpret_cast<f4u *>(f.u_star + ku) = (f4u){us[0], us[1], us[2], us[3]};
+                        } else {                    // four dword stores
+                            f.u_star[ku] = us[0];
+                            f.u_star[ku + 1] = us[1];
+                            f.u_star[ku + 2] = us[2];
+                            f.u_star[ku + 3] = us[3];
+                        }
+                    }
                     const float rdx = g->r_dx, rdy = g->r_dy, dx = g->dx, dy = g->dy;
                     float4 rh;
                     rh.x = (sdiv<SP>(us[1] - us[0], dx, rdx) + sdiv<SP>(vn[0] - vs[0], dy, rdy)) / dt;
