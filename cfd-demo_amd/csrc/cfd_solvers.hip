@@ -471,7 +471,10 @@ constexpr int kSmW = 256;                  // window columns = threads per block
 constexpr int kSmOW = kSmW - 2 * kSmT;     // output columns per block
 // output rows per block: tall tiles (less halo recompute) on big levels,
 // short ones (shorter serial row march per block) on small levels
-constexpr int kSmTHBig = 30, kSmTHSmall = 14;
+#ifndef CFD_MG_TH_BIG
+#define CFD_MG_TH_BIG 30
+#endif
+constexpr int kSmTHBig = CFD_MG_TH_BIG, kSmTHSmall = 14;
 
 template <int FAST, int kSmTH>
 __global__ __launch_bounds__(kSmW) void k_mg_smooth5(MgLevel L, const float *__restrict__ src,
