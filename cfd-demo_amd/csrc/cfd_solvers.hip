@@ -434,17 +434,27 @@ __device__ __forceinline__ void mg_restrict_cell(const MgLevel &F, const MgLevel
 
 // mgProlongate (index.html:1398-1421) of the coarse error e, added to p
 // (:1464-1466): p = f32(p + f32(bilinear)).
-__device__ __forceinline__ float mg_prolong_add_val(const MgLevel &Cl, const float *__restrict__ e,
-                                                    float p_old, int i, int j) {
+// the four coarse values of fine cell (i, j)'s bilinear stencil
+struct ProlongIn {
+    float e00, e01, e10, e11;
+};
+__device__ __forceinline__ ProlongIn mg_prolong_load(const MgLevel &Cl, const float *__restrict__ e,
+                                                     int i, int j) {
     const int nxc = Cl.nx, nyc = Cl.ny;
     const int j0 = j >> 1, i0 = i >> 1;
     const int j1 = min(j0 + 1, nyc - 1), i1 = min(i0 + 1, nxc - 1);
+    return {e[(long)j0 * nxc + i0], e[(long)j0 * nxc + i1], e[(long)j1 * nxc + i0],
+            e[(long)j1 * nxc + i1]};
+}
+__device__ __forceinline__ float mg_prolong_combine(const ProlongIn &q, float p_old, int i, int j) {
     const double b = (j & 1) ? 0.5 : 0.0, a = (i & 1) ? 0.5 : 0.0;
-    const double val = (1 - a) * (1 - b) * (double)e[(long)j0 * nxc + i0] +
-                       a * (1 - b) * (double)e[(long)j0 * nxc + i1] +
-                       (1 - a) * b * (double)e[(long)j1 * nxc + i0] +
-                       a * b * (double)e[(long)j1 * nxc + i1];
+    const double val = (1 - a) * (1 - b) * (double)q.e00 + a * (1 - b) * (double)q.e01 +
+                       (1 - a) * b * (double)q.e10 + a * b * (double)q.e11;
     return (float)((double)p_old + (double)(float)val);
+}
+__device__ __forceinline__ float mg_prolong_add_val(const MgLevel &Cl, const float *__restrict__ e,
+                                                    float p_old, int i, int j) {
+    return mg_prolong_combine(mg_prolong_load(Cl, e, i, j), p_old, i, j);
 }
 
 __device__ __forceinline__ void mg_prolong_add_cell(const MgLevel &Cl, const float *__restrict__ e,
@@ -614,6 +624,110 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *
         for (int y = kHL; y < kH - kHL; ++y) {
             const int gy = gy0 + y;
             if (gy < ny) dst[(long)gy * nx + gx] = c[y];
+        }
+    }
+}
+
+// The same five sweeps (and the PRO / RES fusions) as a register-ring row
+// march: a wave owns a 64-column strip and kMgSlots consecutive input rows;
+// stage s (1..5) of slot t computes row t - 2s of sweep s from the rows sweep
+// s-1 finished in the three earlier slots (lag 2: the five updates of a slot
+// are independent, so one wave has five-way ILP).  A row of each sweep is
+// computed once per strip instead of once per overlapping window, so the
+// vertical halo recompute of k_mg_smooth5w (10 rows per 30) shrinks to the
+// march's warm-up (15-17 slots per 128).  Every update is mg_smooth_cell's
+// expression and every stored value is computed from exact inputs: stage s
+// of row u is exact for u >= s (the rows below are the real field, clamped
+// loads only past the grid), the halo columns as in k_mg_smooth5w.
+constexpr int kMgSlots = 128;    // slots per wave (multiple of kMgU)
+constexpr int kMgU = 16;         // slot unroll: W rings of 4, rhs ring of 16
+constexpr int kMgPD = 4;         // prefetch distance of p and rhs rows
+template <bool RES>
+constexpr int mg_march_rows() { return kMgSlots - (RES ? 17 : 15); }
+
+template <int FAST, bool PRO, bool RES>
+__global__ __launch_bounds__(kBlock) void k_mg_smooth5m(MgLevel L, const float *__restrict__ src,
+                                                        float *__restrict__ dst, const Ctl *ctl,
+                                                        int pass, int nwx, int nwin, MgLevel Cl,
+                                                        const float *__restrict__ e) {
+    constexpr int kHL = kSmT + (RES ? 1 : 0);
+    constexpr int kOW = 64 - 2 * kHL;
+    constexpr int R = mg_march_rows<RES>();
+    constexpr int NS = kSmT + 1;                 // stage rings (0 = input)
+    if (pass_off(ctl, pass)) return;
+    const int lane = (int)threadIdx.x & 63;
+    const int win = (int)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    if (win >= nwin) return;   // wave-uniform
+    const int nx = L.nx, ny = L.ny;
+    const int gx = (win % nwx) * kOW - kHL + lane;
+    const int r0 = (win / nwx) * R;              // first output row
+    const int ra = r0 - kHL;                     // row of slot 0
+    const bool col_in = gx >= 0 && gx < nx;
+    const bool bcol = gx == 0 || gx == nx - 1;
+    const bool out = col_in && lane >= kHL && lane < 64 - kHL;
+    const int gxc = min(max(gx, 0), nx - 1);
+    const float *__restrict__ ps = src + gxc;
+    const float *__restrict__ prh = L.rhs + gxc;
+    float W[NS][4];
+    float RH[kMgU];
+    float PQ[4];
+    ProlongIn EQ[4];
+    auto rowc = [&](int u) { return min(max(ra + u, 0), ny - 1); };
+#pragma unroll
+    for (int u = 0; u < kMgPD; ++u) {
+        const int gy = rowc(u);
+        PQ[u] = ps[(long)gy * nx];
+        if (PRO) EQ[u] = mg_prolong_load(Cl, e, gxc, gy);
+        RH[u] = prh[(long)gy * nx];
+    }
+    for (int base = 0; base < kMgSlots; base += kMgU) {
+#pragma unroll
+        for (int j = 0; j < kMgU; ++j) {
+            const int t = base + j;
+            // input row t (stage 0), then the prefetch of row t + kMgPD
+            {
+                const int gy = rowc(t);
+                W[0][j % 4] = PRO ? mg_prolong_combine(EQ[j % 4], PQ[j % 4], gxc, gy) : PQ[j % 4];
+                const int gp = rowc(t + kMgPD);
+                PQ[j % 4] = ps[(long)gp * nx];
+                if (PRO) EQ[j % 4] = mg_prolong_load(Cl, e, gxc, gp);
+                RH[(j + kMgPD) % kMgU] = prh[(long)gp * nx];
+            }
+#pragma unroll
+            for (int st = 1; st <= kSmT; ++st) {
+                const int u = t - 2 * st;            // row of this stage
+                const int x = ra + u;
+                const float up = W[st - 1][(j - 2 * st + 1 + 64) % 4];
+                const float c = W[st - 1][(j - 2 * st + 64) % 4];
+                const float dn = W[st - 1][(j - 2 * st - 1 + 64) % 4];
+                const float left = from_left(c), right = from_right(c);
+                const double h = ddiv<FAST>((double)right + (double)left, L.dx2, L.r_dx2);
+                const double vt = ddiv<FAST>((double)up + (double)dn, L.dy2, L.r_dy2);
+                const float nv = (float)ddiv<FAST>(h + vt - (double)RH[(j - 2 * st + 64) % kMgU],
+                                                  L.denom, L.r_denom);
+                W[st][(j - 2 * st + 64) % 4] = (bcol || x <= 0 || x >= ny - 1) ? c : nv;
+            }
+            {
+                // sweep 5 of row t - 10 is final
+                const int u = t - 2 * kSmT, x = ra + u;
+                if (out && u >= kHL && u < kHL + R && x < ny)
+                    dst[(long)x * nx + gx] = W[kSmT][(j - 2 * kSmT + 64) % 4];
+            }
+            if (RES) {
+                // residual of row t - 11 from sweep 5's rows t - 12 .. t - 10
+                const int u = t - 2 * kSmT - 1, x = ra + u;
+                const float c = W[kSmT][(j - 2 * kSmT - 1 + 64) % 4];
+                const float up = W[kSmT][(j - 2 * kSmT + 64) % 4];
+                const float dn = W[kSmT][(j - 2 * kSmT - 2 + 64) % 4];
+                const float left = from_left(c), right = from_right(c);
+                const double ap = ddiv<FAST>((double)right + (double)left, L.dx2, L.r_dx2) +
+                                  ddiv<FAST>((double)up + (double)dn, L.dy2, L.r_dy2) -
+                                  L.denom * (double)c;
+                const float r = (bcol || x <= 0 || x >= ny - 1)
+                                    ? 0.0f
+                                    : (float)((double)RH[(j - 2 * kSmT - 1 + 64) % kMgU] - ap);
+                if (out && u >= kHL && u < kHL + R && x < ny) L.r[(long)x * nx + gx] = r;
+            }
         }
     }
 }
@@ -824,17 +938,41 @@ void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl 
         hipLaunchKernelGGL(k_mg_smooth<0>, dim3(g), dim3(kBlock), 0, s, L, src, dst, ctl, pass, nbx);
 }
 
-bool mg_smooth_wave_form() {
-    // CFD_MG_SMOOTH=1: the LDS block form; default: one wave per window
-    static const bool lds_form = [] {
-        const char *e = getenv("CFD_MG_SMOOTH");
-        return e && atoi(e) == 1;
-    }();
-    return !lds_form;
+static int mg_smooth_mode() {
+    // CFD_MG_SMOOTH: 1 the LDS block form, 2 the row march on every level,
+    // 3 the wave windows on every level, 4 the march on big levels only;
+    // default (0): as 4 (4096^2 solve: windows 2.21, march everywhere 1.96,
+    // march on big levels 1.89 ms; profiles/r2/mg/mgm2.log)
+    // read per launch (a few per V-cycle level) so tests can switch forms
+    const char *e = getenv("CFD_MG_SMOOTH");
+    return e ? atoi(e) : 0;
+}
+
+bool mg_smooth_wave_form() { return mg_smooth_mode() != 1; }
+
+// the row march for this level?
+static bool mg_use_march(const MgLevel &L) {
+    const int m = mg_smooth_mode();
+    if (m == 2) return true;
+    return (m == 0 || m == 4) && (long)L.nx * L.ny >= (1L << 23);
+}
+
+template <bool PRO, bool RES>
+static void launch_mg_march(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
+                            const MgLevel &Cl, const float *e, hipStream_t s) {
+    constexpr int kHL = kSmT + (RES ? 1 : 0);
+    const int nwx = cdiv(L.nx, 64 - 2 * kHL);
+    const int nwin = nwx * cdiv(L.ny, mg_march_rows<RES>());
+    const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
+    if (L.fast)
+        hipLaunchKernelGGL((k_mg_smooth5m<1, PRO, RES>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, Cl, e);
+    else
+        hipLaunchKernelGGL((k_mg_smooth5m<0, PRO, RES>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, Cl, e);
 }
 
 void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel &L, const float *src,
                                float *dst, const Ctl *ctl, int pass, hipStream_t s) {
+    if (mg_use_march(L)) return launch_mg_march<true, false>(L, src, dst, ctl, pass, Cl, e, s);
     const bool big = (long)L.nx * L.ny >= (1L << 23);
     const int nwx = cdiv(L.nx, 64 - 2 * kSmT);
     const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
@@ -854,6 +992,7 @@ void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel 
 
 void launch_mg_smooth5_residual(const MgLevel &L, const float *src, float *dst, const Ctl *ctl,
                                 int pass, hipStream_t s) {
+    if (mg_use_march(L)) return launch_mg_march<false, true>(L, src, dst, ctl, pass, L, nullptr, s);
     const bool big = (long)L.nx * L.ny >= (1L << 23);
     const int nwx = cdiv(L.nx, 64 - 2 * (kSmT + 1));
     const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
@@ -873,6 +1012,8 @@ void launch_mg_smooth5_residual(const MgLevel &L, const float *src, float *dst, 
 
 void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl *ctl, int pass,
                        hipStream_t s) {
+    if (mg_smooth_wave_form() && mg_use_march(L))
+        return launch_mg_march<false, false>(L, src, dst, ctl, pass, L, nullptr, s);
     if (mg_smooth_wave_form()) {
         const bool big = (long)L.nx * L.ny >= (1L << 23);
         const int nwx = cdiv(L.nx, 64 - 2 * kSmT);

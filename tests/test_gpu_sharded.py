@@ -239,14 +239,17 @@ def test_sharded_sor_matches_oracle(n, tol, depth):
                                         tol_enabled=int(tol)), 4, FIELDS + ("rhs",))
 
 
-@pytest.mark.parametrize("n,tol", [(2, False), (3, True), (4, False)])
-def test_sharded_multigrid_matches_oracle(n, tol):
+@pytest.mark.parametrize("n,tol,smooth", [(2, False, None), (3, True, None), (4, False, None),
+                                          (3, False, "2")])
+def test_sharded_multigrid_matches_oracle(monkeypatch, n, tol, smooth):
     """Multigrid (pressure_solver 2) on slabs: the rhs is gathered to every
     rank, the whole grid is solved redundantly with the single-domain kernels
     and each slab keeps its rows (plus exact deep ghosts): bitwise against the
     single-domain oracle, fixed and tolerance (host-driven) modes, cylinder
     across a slab boundary, corrector passes."""
     import cfdamd
+    if smooth is not None:
+        monkeypatch.setenv("CFD_MG_SMOOTH", smooth)   # 2: the row-march smoother
     grid = cfdamd.Grid(128, 96, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.9))
     params = cfdamd.SimulationParams(pressure_solver=cfdamd.PressureSolver.Multigrid,
                                      corrector_passes=3, tol_enabled=tol)

@@ -35,13 +35,17 @@ def _oracle(nx, ny, lx, ly, cylinder=None, **p):
     return OracleModel(nx, ny, lx, ly, cylinder=cylinder, **p)
 
 
-@pytest.mark.parametrize("tail,tb", [("default", "1"), ("0", "1"), ("100000000", "1"),
-                                     ("0", "0")])
+@pytest.mark.parametrize("tail,tb,smooth", [("default", "1", None), ("0", "1", None),
+                                            ("100000000", "1", None), ("0", "0", None),
+                                            ("0", "1", "2"), ("0", "1", "1")])
 @pytest.mark.parametrize("name", sorted(JS))
-def test_multigrid_solve_matches_reference_javascript(monkeypatch, name, tail, tb):
+def test_multigrid_solve_matches_reference_javascript(monkeypatch, name, tail, tb, smooth):
     """tail: levels run in the single-workgroup tail (0: only the coarsest);
-    tb: five smoothing sweeps per launch through LDS (1) or one per launch (0)."""
+    tb: five smoothing sweeps per launch (1) or one per launch (0); smooth:
+    CFD_MG_SMOOTH (2: the row march on every level, 1: the LDS block form)."""
     c = _cfd()
+    if smooth is not None:
+        monkeypatch.setenv("CFD_MG_SMOOTH", smooth)
     if tail != "default":
         monkeypatch.setenv("CFD_MG_TAIL", tail)
     monkeypatch.setenv("CFD_MG_TB", tb)
@@ -146,10 +150,15 @@ def test_switching_solvers_mid_run():
         assert_bitwise(f, st[f], o.field(f))
 
 
+@pytest.mark.parametrize("smooth", ["default", "2", "3"])
 @pytest.mark.parametrize("nx,ny,lx,ly", [(1024, 1024, 1.0, 1.0), (1048, 1000, 30.0, 10.0)])
-def test_multigrid_large_grids_match_oracle(nx, ny, lx, ly):
+def test_multigrid_large_grids_match_oracle(monkeypatch, nx, ny, lx, ly, smooth):
     """Grids of >= 2^20 cells: deep hierarchies, many smoothing tiles and deep
-    hierarchies (power-of-two divisors and IEEE double division)."""
+    hierarchies (power-of-two divisors and IEEE double division).  smooth:
+    CFD_MG_SMOOTH (2: the row march k_mg_smooth5m on every level, 3: the wave
+    windows k_mg_smooth5w on every level)."""
+    if smooth != "default":
+        monkeypatch.setenv("CFD_MG_SMOOTH", smooth)
     c = _cfd()
     import oracle
     rng = np.random.default_rng(nx)
