@@ -172,3 +172,25 @@ def test_multigrid_large_grids_match_oracle(monkeypatch, nx, ny, lx, ly, smooth)
     r2 = oracle.mg_solve(want, rhs, nx, ny, dx, dy)
     assert_bitwise(f"mg {nx}x{ny}", m.get_state()["p_prime"], want)
     assert np.float32(r) == np.float32(r2)
+
+
+def test_multigrid_march_on_big_level_matches_windows(monkeypatch):
+    """The default smoother form on a level of >= 2^23 cells is the row march
+    (k_mg_smooth5m); it must give the same bits as the wave-window form
+    (CFD_MG_SMOOTH=3), which the oracle tests above pin at smaller sizes (and
+    the march too, under CFD_MG_SMOOTH=2)."""
+    c = _cfd()
+    nx, ny = 4096, 2048
+    rng = np.random.default_rng(7)
+    rhs = (rng.uniform(-1, 1, nx * ny) * 50.0).astype(np.float32)
+    out = {}
+    for smooth in ("0", "3"):
+        monkeypatch.setenv("CFD_MG_SMOOTH", smooth)
+        m = c.Model(c.Grid(nx, ny, 2.0, 1.0),
+                    c.SimulationParams(pressure_solver=c.PressureSolver.Multigrid))
+        m.set_state(rhs=rhs)
+        r = m.pressure_solve()
+        out[smooth] = (m.get_state()["p_prime"], np.float32(r))
+        m.close()
+    assert_bitwise("march vs windows 4096x2048", out["0"][0], out["3"][0])
+    assert out["0"][1] == out["3"][1]
