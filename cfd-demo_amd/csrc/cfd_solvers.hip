@@ -639,7 +639,10 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *
 // expression and every stored value is computed from exact inputs: stage s
 // of row u is exact for u >= s (the rows below are the real field, clamped
 // loads only past the grid), the halo columns as in k_mg_smooth5w.
-constexpr int kMgSlots = 128;    // slots per wave (multiple of kMgU)
+#ifndef CFD_MG_SLOTS
+#define CFD_MG_SLOTS 128
+#endif
+constexpr int kMgSlots = CFD_MG_SLOTS;   // slots per wave (multiple of kMgU)
 constexpr int kMgU = 16;         // slot unroll: W rings of 4, rhs ring of 16
 constexpr int kMgPD = 4;         // prefetch distance of p and rhs rows
 template <bool RES>
