@@ -943,9 +943,11 @@ void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl 
 
 static int mg_smooth_mode() {
     // CFD_MG_SMOOTH: 1 the LDS block form, 2 the row march on every level,
-    // 3 the wave windows on every level, 4 the march on big levels only;
-    // default (0): as 4 (4096^2 solve: windows 2.21, march everywhere 1.96,
-    // march on big levels 1.89 ms; profiles/r2/mg/mgm2.log)
+    // 3 the wave windows on every level, 4 the march on levels of at least
+    // 2^CFD_MG_MARCH_MIN cells (default 22) and the windows below; default
+    // (0): as 4 (4096^2 solve: windows 2.21, march everywhere 1.96, march
+    // from 2^23 1.90, from 2^22 1.70, from 2^21 1.71 ms;
+    // profiles/r2/mg/mgm2.log, mg_min_ab.log)
     // read per launch (a few per V-cycle level) so tests can switch forms
     const char *e = getenv("CFD_MG_SMOOTH");
     return e ? atoi(e) : 0;
@@ -957,7 +959,9 @@ bool mg_smooth_wave_form() { return mg_smooth_mode() != 1; }
 static bool mg_use_march(const MgLevel &L) {
     const int m = mg_smooth_mode();
     if (m == 2) return true;
-    return (m == 0 || m == 4) && (long)L.nx * L.ny >= (1L << 23);
+    const char *mn = getenv("CFD_MG_MARCH_MIN");   // log2 cells of the smallest march level
+    const int lg = mn ? atoi(mn) : 22;
+    return (m == 0 || m == 4) && (long)L.nx * L.ny >= (1L << lg);
 }
 
 template <bool PRO, bool RES>

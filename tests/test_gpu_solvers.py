@@ -175,7 +175,7 @@ def test_multigrid_large_grids_match_oracle(monkeypatch, nx, ny, lx, ly, smooth)
 
 
 def test_multigrid_march_on_big_level_matches_windows(monkeypatch):
-    """The default smoother form on a level of >= 2^23 cells is the row march
+    """The default smoother form on a level of >= 2^22 cells is the row march
     (k_mg_smooth5m); it must give the same bits as the wave-window form
     (CFD_MG_SMOOTH=3), which the oracle tests above pin at smaller sizes (and
     the march too, under CFD_MG_SMOOTH=2)."""
