@@ -28,6 +28,11 @@ reports the 12 B x cells x T figure separately.  At N=1 a second entry,
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`--gpus N` with N > 1 and no external launcher (WORLD_SIZE unset): this
+process spawns the N ranks itself (one child per GPU, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT set) before anything touches the GPU,
+and prints rank 0's JSON line; it never measures fewer ranks than asked.
 """
 import argparse
 import json
@@ -109,13 +114,13 @@ def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=5):
                         f"{1e3 * max(times):.0f}); host {model}, {ncpu} cpus"}
 
 
-def oracle_from_state(nx, ny, iters, re, state, threads):
+def oracle_from_state(nx, ny, iters, re, state, threads, scheme=0, passes=0, tol=0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from oracle import OracleModel
     orc.set_threads(threads)
     m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
-                    jacobi_iters=iters, corrector_passes=0, tol_enabled=0)
+                    jacobi_iters=iters, corrector_passes=passes, tol_enabled=tol, scheme=scheme)
     for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
         m.field(k)[:] = state[k]
     sc = m.scalars()
@@ -125,11 +130,11 @@ def oracle_from_state(nx, ny, iters, re, state, threads):
     return m, orc
 
 
-def parity_developed_step(model, nx, ny, iters, re, state, threads):
+def parity_developed_step(model, nx, ny, iters, re, state, threads, **mode):
     """One GPU step and one oracle step from the same developed state; True
     when every field word and every scalar agree."""
     import numpy as np
-    o, orc = oracle_from_state(nx, ny, iters, re, state, threads)
+    o, orc = oracle_from_state(nx, ny, iters, re, state, threads, **mode)
     model.update()
     o.update()
     orc.set_threads(1)
@@ -141,7 +146,98 @@ def parity_developed_step(model, nx, ny, iters, re, state, threads):
                     ("last_v_residual", s.v), ("simulation_time", s.time)):
         if np.float32(g[k]).view(np.uint32) != np.float32(want).view(np.uint32):
             bad.append(k)
+    if int(g["jacobi_sweeps_total"]) != int(s.jacobi_sweeps_total):
+        bad.append("jacobi_sweeps_total")
     return not bad, bad
+
+
+def phase_window(model, steps):
+    """Per-phase device time of `steps` more steps (a separate window after
+    the timed one: the extra event records would perturb the headline)."""
+    model.synchronize()
+    model.timing_phases(True)
+    model.timing_begin()
+    model.update_n(steps)
+    tm = model.timing_end()
+    ph = model.timing_phase_ms()
+    model.timing_phases(False)
+    k = max(tm["steps"], 1)
+    return {"steps": k, "predict_march_us": 1e3 * ph["predict_ms"] / k,
+            "correct_finish_us": 1e3 * ph["finish_ms"] / k,
+            "solve_us": 1e3 * tm["solve_ms"] / k, "step_us_events": 1e3 * tm["step_ms"] / k}
+
+
+def so_leg(args, cfdamd, device, nx, ny, steps=10):
+    """The same timed-mode step with second-order upwind advection
+    (VelocityScheme::SecondOrder, model.rs:910-1053, 1097-1248): developed
+    like the headline run, timed, per-phase times, and one step bitwise
+    against the oracle from the developed state."""
+    params = cfdamd.SimulationParams.cavity(
+        args.re, args.iters, corrector_passes=0, tol_enabled=False,
+        velocity_scheme=cfdamd.VelocityScheme.SecondOrder)
+    model = cfdamd.Model(cfdamd.cavity_grid(nx, ny), params, device=device)
+    model.update_n(args.develop + args.warmup)
+    model.synchronize()
+    t0 = time.perf_counter()
+    model.update_n(steps)
+    model.synchronize()
+    el = time.perf_counter() - t0
+    out = {"workload": f"{nx}x{ny} cavity Re={args.re:g}, SecondOrder upwind, {args.iters} "
+                       f"sweeps/step, tolerance off, developed {args.develop} steps",
+           "steps": steps, "ms_per_step": 1e3 * el / steps,
+           "value": nx * ny * args.iters * steps / el, "unit": "cell-updates/s",
+           "phases": phase_window(model, 5)}
+    if not args.no_parity:
+        state = model.get_state()
+        ok, bad = parity_developed_step(model, nx, ny, args.iters, args.re, state, cpu_threads(),
+                                        scheme=1)
+        out["parity_developed_step"] = ok
+        if not ok:
+            out["parity_differ"] = bad
+    model.close()
+    return out
+
+
+def parity_mode_leg(args, cfdamd, device, n, re, fixed_iters, steps=5):
+    """The reference's own control flow (model.rs:696-724, 748-819): 50-sweep
+    solves with the 1e-4 early exit and up to 20 re-correction passes.  The
+    cavity is developed in the fixed-count mode (args.develop steps), its state
+    injected into a model with the reference's parameters, then 2 warm-up and
+    `steps` timed steps; sweeps/step counts the sweeps the reference's loop
+    runs (early exits included).  One more step is compared bitwise with the
+    oracle in the same mode."""
+    grid = cfdamd.cavity_grid(n)
+    dev = cfdamd.Model(grid, cfdamd.SimulationParams.cavity(
+        re, fixed_iters, corrector_passes=0, tol_enabled=False), device=device)
+    dev.update_n(args.develop)
+    st = dev.get_state()
+    dev.close()
+    ref = cfdamd.SimulationParams.cavity(re, 50)   # jacobi 50, passes 20, tol 1e-4
+    m = cfdamd.Model(grid, ref, device=device)
+    m.set_state(**st)
+    m.update_n(2)
+    s0 = m.get_residuals().jacobi_sweeps_total
+    m.synchronize()
+    t0 = time.perf_counter()
+    m.update_n(steps)
+    m.synchronize()
+    el = time.perf_counter() - t0
+    sweeps = m.get_residuals().jacobi_sweeps_total - s0
+    out = {"workload": f"{n}x{n} cavity Re={re:g}, reference control flow: <=50 sweeps/solve, "
+                       f"early exit at 1e-4, <=20 corrector passes (model.rs:696-724, 748-819)",
+           "developed": f"{args.develop} fixed-count steps ({fixed_iters} sweeps), state injected",
+           "kernel": m.jacobi_kernel["name"],
+           "steps": steps, "ms_per_step": 1e3 * el / steps, "sweeps_per_step": sweeps / steps,
+           "cell_updates_per_s": n * n * sweeps / el,
+           "us_per_sweep": 1e6 * el / max(sweeps, 1)}
+    if not args.no_parity:
+        state = m.get_state()
+        ok, bad = parity_developed_step(m, n, n, 50, re, state, cpu_threads(), passes=20, tol=1)
+        out["parity_developed_step"] = ok
+        if not ok:
+            out["parity_differ"] = bad
+    m.close()
+    return out
 
 
 def time_jacobi(model, steps):
@@ -249,6 +345,72 @@ def control_run(args, cfdamd, device, n=8192, steps=10):
     return e
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, timeout_s):
+    """`--gpus N` without an external launcher: run N copies of this script,
+    one rank per GPU, and relay rank 0's JSON line.  The parent never loads
+    the HIP library or torch's GPU runtime (children are separate processes,
+    never exec'd from a process that touched the GPU).  A rank that fails
+    ends the job: the others are terminated and the exit status is non-zero."""
+    import threading
+    port = free_port()
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   CFD_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+            stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+
+    def relay():
+        for line in procs[0].stdout:
+            lines.append(line)
+            sys.stdout.write(line)
+            sys.stdout.flush()
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    t_end = time.monotonic() + timeout_s
+    rcs = [None] * n
+    failed = None
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0) and failed is None:
+                    failed = r
+        if failed is not None or time.monotonic() > t_end:
+            break
+        time.sleep(0.2)
+    if failed is not None or any(rc is None for rc in rcs):
+        why = (f"rank {failed} exited with status {rcs[failed]}" if failed is not None
+               else f"ranks still running after {timeout_s:.0f} s")
+        print(f"bench.py launcher: {why}; terminating the other ranks", file=sys.stderr,
+              flush=True)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        th.join(timeout=5)
+        raise SystemExit(1)
+    th.join(timeout=30)
+    if not any(l.lstrip().startswith("{") for l in lines):
+        print("bench.py launcher: rank 0 printed no JSON line", file=sys.stderr, flush=True)
+        raise SystemExit(1)
+    raise SystemExit(max(rcs))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,8 +433,19 @@ def main():
     ap.add_argument("--no-control", action="store_true",
                     help="skip the 8192^2 (non-MALL-resident) roofline control at N=1")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-so", action="store_true",
+                    help="skip the second-order upwind leg at N=1")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="skip the reference-control-flow legs (C2, C3) at N=1")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="seconds the self-launched ranks of --gpus N may take")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher and rank plumbing only (gloo, no GPU, no HIP library): "
+                         "prints a line with dry_run true and no measurement")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args.gpus, args.launch_timeout)   # does not return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -286,7 +459,7 @@ def main():
         os.environ.setdefault("NCCL_NET", "Socket")
         local = 0
     n = max(world, 1)
-    if args.gpus != n and world > 1:
+    if args.gpus != n:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
 
     dist = None
@@ -294,7 +467,24 @@ def main():
         import torch
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    launcher = os.environ.get("CFD_BENCH_LAUNCHER", "external" if world > 1 else "none")
+    if args.dry_run:
+        ranks = dist.get_world_size() if dist is not None else 1
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s",
+                              "n_gpus": n, "ranks_seen": ranks, "launcher": launcher,
+                              "dry_run": True}), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     import cfdamd
+    if world > 1 and os.environ.get("CFD_BENCH_LOOPBACK") != "1":
+        ndev = cfdamd.device_count()
+        if ndev < world or local >= ndev:
+            print(f"bench.py rank {rank}: --gpus {world} needs {world} GPUs, this process sees "
+                  f"{ndev}", file=sys.stderr, flush=True)
+            raise SystemExit(3)
 
     nx, ny = global_grid(n)
     if args.nx:
@@ -334,11 +524,13 @@ def main():
     barrier()
     tm = model.timing_end()
     elapsed = t1 - t0
+    rank_elapsed = [elapsed]
     if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, elapsed)
+        rank_elapsed = [float(x) for x in gathered]
+        elapsed = max(rank_elapsed)
+    ranks_seen = model.comm_size
 
     import numpy as np
     try:
@@ -366,6 +558,9 @@ def main():
             "value": nx * ny * args.iters * args.steps / elapsed,
             "unit": "cell-updates/s",
             "n_gpus": n,
+            "ranks_seen": ranks_seen,
+            "launcher": launcher,
+            "rank_ms_per_step": [1e3 * e / args.steps for e in rank_elapsed],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
@@ -413,6 +608,14 @@ def main():
                 f"1 step from step {state['simulation_step']} on GPU and oracle "
                 f"(oracle/cfd_oracle.c), every word of u, v, p, u*, v*, p', rhs and the "
                 f"scalars compared" + ("" if ok else f"; differ: {bad}"))
+        if n == 1:
+            out["phases"] = phase_window(model, 5)
+        if n == 1 and not args.no_so:
+            out["so_step"] = so_leg(args, cfdamd, local, nx, ny)
+        if n == 1 and not args.no_parity_mode:
+            out["parity_mode"] = {
+                "C2": parity_mode_leg(args, cfdamd, local, 1024, 400.0, 100),
+                "C3": parity_mode_leg(args, cfdamd, local, 4096, 1000.0, 200)}
         if n == 1 and not args.no_control:
             out["roofline_control"] = control_run(args, cfdamd, local)
         if n == 1 and not args.no_cpu_baseline:

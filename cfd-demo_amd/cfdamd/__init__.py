@@ -30,7 +30,7 @@ from ._lib import (CFD_ENONFINITE, CfdError, CfdGrid, CfdParams, CfdResiduals, C
 __all__ = [
     "VelocityScheme", "InletProfile", "PressureSolver", "BoundaryKind", "Cylinder", "Grid",
     "SimulationParams", "Residuals", "SimSnapshot", "Model", "SimulationControlHandle",
-    "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "load", "LocalHub",
+    "CfdError", "default_grid", "cavity_grid", "rccl_unique_id", "device_count", "load", "LocalHub",
     "VisualizationMode", "CFD_ENONFINITE",
 ]
 
@@ -167,6 +167,13 @@ class LocalHub:
         if self.handle:
             load().cfd_local_hub_destroy(self.handle)
             self.handle = None
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (cfd_device_count)."""
+    n = C.c_int()
+    check("cfd_device_count", load().cfd_device_count(C.byref(n)))
+    return int(n.value)
 
 
 def rccl_unique_id() -> bytes:
@@ -335,6 +342,16 @@ class Model:
         return {"solve_ms": a.value, "sweeps": int(b.value), "step_ms": c.value,
                 "steps": int(d.value)}
 
+    def timing_phases(self, on: bool = True) -> None:
+        """Also time the predictor and finish phases in timing windows."""
+        check("cfd_timing_phases", load().cfd_timing_phases(self._hh(), 1 if on else 0))
+
+    def timing_phase_ms(self) -> dict:
+        a, b = C.c_double(), C.c_double()
+        check("cfd_timing_phase_ms",
+              load().cfd_timing_phase_ms(self._hh(), C.byref(a), C.byref(b)))
+        return {"predict_ms": a.value, "finish_ms": b.value}
+
     @property
     def kernel_config(self) -> dict:
         fd, tb = C.c_int(), C.c_int()
@@ -382,6 +399,13 @@ class Model:
         check("cfd_get_jacobi_kernel",
               load().cfd_get_jacobi_kernel(self._hh(), C.byref(kind), name, 96))
         return {"kind": kind.value, "name": name.value.decode()}
+
+    @property
+    def comm_size(self) -> int:
+        """Ranks the transport reports (ncclCommCount; LocalHub size; 1)."""
+        n = C.c_int()
+        check("cfd_get_comm_size", load().cfd_get_comm_size(self._hh(), C.byref(n)))
+        return int(n.value)
 
     @property
     def halo_depth(self) -> int:

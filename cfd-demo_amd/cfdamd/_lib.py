@@ -15,10 +15,11 @@ LIB_PATH = os.environ.get("CFD_LIB") or os.path.join(ROOT, "lib", "libcfd_amd.so
 EXPORTS = [
     "cfd_default_params", "cfd_default_grid", "cfd_create", "cfd_rccl_unique_id",
     "cfd_create_sharded", "cfd_local_hub_create", "cfd_local_hub_destroy",
-    "cfd_create_sharded_local", "cfd_get_slab", "cfd_update", "cfd_update_n", "cfd_piso_step",
+    "cfd_create_sharded_local", "cfd_device_count", "cfd_get_comm_size", "cfd_get_slab", "cfd_update", "cfd_update_n", "cfd_piso_step",
     "cfd_pressure_solve", "cfd_run_phase", "cfd_set_params", "cfd_get_snapshot",
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
-    "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_get_halo_depth",
+    "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_timing_phases",
+    "cfd_timing_phase_ms", "cfd_get_halo_depth",
     "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block", "cfd_plan_overlap",
     "cfd_render", "cfd_derive_field", "cfd_last_error", "cfd_abi_version", "cfd_destroy",
     "cfd_get_config", "cfd_run_start", "cfd_run_stop", "cfd_run_pause", "cfd_run_resume",
@@ -111,6 +112,8 @@ def load():
         "cfd_local_hub_destroy": (None, [vp]),
         "cfd_create_sharded_local": (i32, [C.POINTER(CfdGrid), C.POINTER(CfdParams), i32, i32,
                                            i32, vp, C.POINTER(vp)]),
+        "cfd_device_count": (i32, [C.POINTER(i32)]),
+        "cfd_get_comm_size": (i32, [vp, C.POINTER(i32)]),
         "cfd_get_slab": (i32, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "cfd_update": (i32, [vp]),
         "cfd_update_n": (i32, [vp, i32]),
@@ -128,6 +131,8 @@ def load():
         "cfd_timing_begin": (i32, [vp]),
         "cfd_timing_end": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+        "cfd_timing_phases": (i32, [vp, i32]),
+        "cfd_timing_phase_ms": (i32, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
         "cfd_get_halo_depth": (i32, [vp]),
         "cfd_get_kernel_config": (i32, [vp, C.POINTER(i32), C.POINTER(i32)]),
         "cfd_get_jacobi_kernel": (i32, [vp, C.POINTER(i32), C.c_char_p, C.c_size_t]),

@@ -113,6 +113,9 @@ struct Fields {
     // host-mapped word (pinned, zero-copy) mirroring Ctl::nonfinite_step, so the
     // host can see a blown-up run without synchronising the stream
     uint32_t *host_nonfinite;
+    // host-mapped word the step finalize sets to Ctl::step (sharded models):
+    // the RCCL watchdog's evidence of forward progress
+    uint32_t *host_progress;
 };
 
 // ---- launchers (cfd_kernels.hip) ----

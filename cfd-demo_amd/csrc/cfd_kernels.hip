@@ -951,6 +951,7 @@ __device__ __forceinline__ void step_finalize_body(const Geom &g, const Fields &
     c->res_v = __uint_as_float(c->red[1]);
     const float max_vel = fmaxf(__uint_as_float(c->red[2]), __uint_as_float(c->red[3]));
     c->step += 1u;
+    if (f.host_progress) *f.host_progress = c->step;   // watchdog progress (zero-copy)
     c->time = c->time + c->dt;
     const float previous_dt = c->dt;
     float new_dt;

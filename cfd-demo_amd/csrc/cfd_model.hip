@@ -50,6 +50,16 @@ int fail(int code, const std::string &msg) {
             return fail(CFD_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));    \
     } while (0)
 
+// An operation on the model's communicator.  The communicator is created
+// non-blocking (so its creation can time out, create_common), which lets any
+// call on it return ncclInProgress: settle() then waits, under the RCCL
+// deadline, until the communicator's state leaves ncclInProgress.
+#define RCCL_OP(expr)                                                                      \
+    do {                                                                                   \
+        int rc_ = settle((expr), #expr);                                                   \
+        if (rc_) return rc_;                                                               \
+    } while (0)
+
 const float kNaN = std::nanf("");
 
 size_t round4(size_t n) { return (n + 3) & ~size_t(3); }
@@ -138,6 +148,19 @@ struct cfd_model {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> solve_events;
+    // per-phase events (cfd_timing_phases): predictors + first divergence,
+    // and the corrector / finish, summed at cfd_timing_end
+    bool timing_phases = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> phase_events[2];
+    double phase_ms[2] = {0.0, 0.0};
+    hipEvent_t phase_mark(int ph, bool end) {
+        if (!(timing && timing_phases)) return nullptr;
+        hipEvent_t e = take_event();
+        (void)hipEventRecord(e, stream);
+        if (end) phase_events[ph].back().second = e;
+        else phase_events[ph].emplace_back(e, nullptr);
+        return e;
+    }
     size_t ev_next = 0;
     uint64_t timed_sweeps = 0, timed_steps = 0, timed_launches = 0;
     double timed_step_ms = 0.0;
@@ -182,7 +205,7 @@ struct cfd_model {
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
         RCCL_TRY(ncclGroupStart());
         int rc = exchange_ops(id, kind, depth, st);
-        RCCL_TRY(ncclGroupEnd());
+        RCCL_OP(ncclGroupEnd());
         return rc;
     }
 
@@ -193,15 +216,15 @@ struct cfd_model {
         int h[6];
         plan_halo(kind, g.nyl, depth, rank, n_ranks, h);
         if (h[2] > 0) {
-            RCCL_TRY(ncclSend(base + (long)h[0] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
+            RCCL_OP(ncclSend(base + (long)h[0] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
                               rank - 1, comm, st));
-            RCCL_TRY(ncclRecv(base + (long)h[1] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
+            RCCL_OP(ncclRecv(base + (long)h[1] * (long)pitch, (size_t)h[2] * pitch, ncclFloat,
                               rank - 1, comm, st));
         }
         if (h[5] > 0) {
-            RCCL_TRY(ncclSend(base + (long)h[3] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
+            RCCL_OP(ncclSend(base + (long)h[3] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
                               rank + 1, comm, st));
-            RCCL_TRY(ncclRecv(base + (long)h[4] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
+            RCCL_OP(ncclRecv(base + (long)h[4] * (long)pitch, (size_t)h[5] * pitch, ncclFloat,
                               rank + 1, comm, st));
         }
         return 0;
@@ -245,7 +268,7 @@ struct cfd_model {
         RCCL_TRY(ncclGroupStart());
         int rc = exchange_ops(FLD_U, HALO_U, 2, st);
         if (!rc) rc = exchange_ops(FLD_V, HALO_V, 2, st);
-        RCCL_TRY(ncclGroupEnd());
+        RCCL_OP(ncclGroupEnd());
         return rc;
     }
 
@@ -271,8 +294,35 @@ struct cfd_model {
             return 0;
         }
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
-        RCCL_TRY(ncclAllReduce(dev, dev, n, ncclUint32, ncclMax, comm, stream));
+        RCCL_OP(ncclAllReduce(dev, dev, n, ncclUint32, ncclMax, comm, stream));
         return 0;
+    }
+
+    // Resolve the result of a call on the (non-blocking) communicator: poll
+    // its asynchronous state while it is ncclInProgress, up to the deadline.
+    int settle(ncclResult_t r, const char *what) {
+        if (r == ncclSuccess) return 0;
+        if (r == ncclInProgress && comm) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (;;) {
+                ncclResult_t st = ncclInProgress;
+                r = ncclCommGetAsyncError(comm, &st);
+                if (r == ncclSuccess) r = st;
+                if (r != ncclInProgress) break;
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+                    rccl_timeout_s) {
+                    ncclCommAbort(comm);
+                    comm = nullptr;
+                    comm_aborted = true;
+                    return fail(CFD_ERCCL, std::string(what) + ": still in progress after " +
+                                               std::to_string((int)rccl_timeout_s) +
+                                               " s; the communicator was aborted");
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+            if (r == ncclSuccess) return 0;
+        }
+        return fail(CFD_ERCCL, std::string(what) + ": " + ncclGetErrorString(r));
     }
 
     // Wait for the stream (ev == nullptr) or for one event, with the RCCL
@@ -284,12 +334,21 @@ struct cfd_model {
             HIP_TRY(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(stream));
             return 0;
         }
-        const auto t0 = std::chrono::steady_clock::now();
+        // the deadline runs from the last forward progress the host saw (a
+        // finished step: the device mirrors Ctl::step into h_nonfinite[1]),
+        // not from the start of the wait, so a long healthy queue never trips it
+        auto t0 = std::chrono::steady_clock::now();
+        uint32_t seen = *(volatile uint32_t *)(h_nonfinite + 1);
         for (int spin = 0;; ++spin) {
             const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(stream);
             if (q == hipSuccess) return 0;
             if (q != hipErrorNotReady)
                 return fail(CFD_EHIP, std::string("stream/event query: ") + hipGetErrorString(q));
+            const uint32_t now_step = *(volatile uint32_t *)(h_nonfinite + 1);
+            if (now_step != seen) {
+                seen = now_step;
+                t0 = std::chrono::steady_clock::now();
+            }
             ncclResult_t ar = ncclSuccess;
             const ncclResult_t r = ncclCommGetAsyncError(comm, &ar);
             const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -579,10 +638,10 @@ struct cfd_model {
             if (r == rank) continue;
             uint64_t a, b;
             plan_slab(g.ny, n_ranks, r, &a, &b);
-            RCCL_TRY(ncclSend(f.rhs, (size_t)g.nyl * nx, ncclFloat, r, comm, stream));
-            RCCL_TRY(ncclRecv(full + a * nx, (size_t)(b - a) * nx, ncclFloat, r, comm, stream));
+            RCCL_OP(ncclSend(f.rhs, (size_t)g.nyl * nx, ncclFloat, r, comm, stream));
+            RCCL_OP(ncclRecv(full + a * nx, (size_t)(b - a) * nx, ncclFloat, r, comm, stream));
         }
-        RCCL_TRY(ncclGroupEnd());
+        RCCL_OP(ncclGroupEnd());
         return 0;
     }
 
@@ -709,10 +768,19 @@ struct cfd_model {
             // the deep-halo sweeps recompute ghost rows, which read rhs there.
             // Overlapped (r2): the rhs exchange runs on cstream while the first
             // launch's interior rows, whose T sweeps read no rhs ghost row
-            // (stage 1 of output rows [a, b) reads rhs rows [a-T+1, b+T-1)),
+            // (the march for output rows [a, b) loads rhs rows [a-T, b+T)),
             // run on stream; the edge rows follow once the ghosts are in.
-            const bool rhs_ovl = overlap && tmax > 1 && !pp_ghosts_shallow;
+            const bool rhs_ovl = overlap && tmax > 1 && !pp_ghosts_shallow && iters > 0;
             bool rhs_pending = false;
+            // whatever path leaves this block, stream waits for the rhs exchange
+            // on cstream (so a sync of stream also covers that RCCL group)
+            struct JoinRhs {
+                cfd_model *m;
+                bool *pending;
+                ~JoinRhs() {
+                    if (*pending) (void)hipStreamWaitEvent(m->stream, m->ev_rhs, 0);
+                }
+            } join_rhs{this, &rhs_pending};
             int rc0;
             if (rhs_ovl) {
                 HIP_TRY(hipEventRecord(ev_ov0, stream));   // rhs written
@@ -736,7 +804,9 @@ struct cfd_model {
                 const int res = it + T == iters;
                 if (rhs_pending) {
                     rhs_pending = false;
-                    const int a = std::max(lo, T - 1), b = std::min(hi, g.nyl - T + 1);
+                    // the kernel's march loads rhs rows [a-T, b+T) (prefetch
+                    // included), so no loaded row is an exchanged ghost row
+                    const int a = std::max(lo, T), b = std::min(hi, g.nyl - T);
                     const bool split = a < b && !exch;
                     if (split) launch_jacobi_block(g, f, pass, it, launches, T, a, b, res, stream);
                     HIP_TRY(hipStreamWaitEvent(stream, ev_rhs, 0));
@@ -895,6 +965,7 @@ struct cfd_model {
         // K1-K3: the fused march when it applies, else predictors + divergence
         const bool march = predict_march_ok(g, f);
         const bool fused = march || predict_div_fused(g, f);
+        phase_mark(0, false);
         if (march && finish && uv_async) {
             // rows [2, nyl-2) read u rows >= 0 and <= nyl-1 and v rows <= nyl;
             // the edge rows (4-row launches overlapping the interior ones:
@@ -911,6 +982,7 @@ struct cfd_model {
             launch_predict(g, f, dt_override, stream);
         auto first_divergence = [&](int pass) {
             if (!fused) launch_divergence(g, f, pass, dt_override, stream);
+            phase_mark(0, true);
         };
         if (finish) {
             first_divergence(host_driven() ? -1 : 0);
@@ -928,8 +1000,10 @@ struct cfd_model {
             merge_res_allreduce = false;
             defer_finalize = false;
             if (rc) return rc;
+            phase_mark(1, false);
             launch_correct_finish(g, f, dt_override, stream, step_finalize_folded,
                                   fin_pending ? &fin_deferred : nullptr);
+            phase_mark(1, true);
             fin_pending = false;
             HIP_TRY(hipGetLastError());
             return 0;
@@ -1096,7 +1170,13 @@ struct cfd_model {
     void destroy() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        if (comm) ncclCommDestroy(comm);
+        if (comm) {
+            // a non-blocking communicator finalises asynchronously: wait (under
+            // the deadline) for it, else abort instead of hanging in destroy
+            if (settle(ncclCommFinalize(comm), "ncclCommFinalize") == 0 && comm)
+                ncclCommDestroy(comm);
+            comm = nullptr;
+        }
         for (hipEvent_t e : ev_res)
             if (e) (void)hipEventDestroy(e);
         if (h_res) (void)hipHostFree(h_res);
@@ -1143,6 +1223,22 @@ int validate(const cfd_grid *grid, const cfd_params *p) {
     if (p->pressure_solver < CFD_SOLVER_JACOBI || p->pressure_solver > CFD_SOLVER_MULTIGRID)
         return fail(CFD_EINVAL, "pressure_solver must be 0 (Jacobi), 1 (SOR) or 2 (multigrid)");
     if (p->bc_kind != 0 && p->bc_kind != 1) return fail(CFD_EINVAL, "bc_kind must be 0 or 1");
+    return 0;
+}
+
+// Sharded SOR (enqueue_sor_sharded) needs >= 1 iteration, halo depth >= 2
+// and >= 16 interior rows in the slab.  Checked wherever the solver can be
+// chosen (create, cfd_set_params, cfd_run_set_params), so a step never fails
+// half-way through with u*, v* and rhs already written.
+int validate_sharded(const cfd_model *m, const cfd_params *p) {
+    if (m->n_ranks <= 1 || p->pressure_solver != CFD_SOLVER_SOR) return 0;
+    const int lo = std::max(0, 1 - (int)m->j0);
+    const int hi = std::min((int)(m->j1 - m->j0), (int)m->grid.ny - 1 - (int)m->j0);
+    if (p->jacobi_iters < 1 || m->g.hg < 2 || !sor_fused_ok((int)m->grid.nx, hi - lo))
+        return fail(CFD_EINVAL, "sharded SOR needs >= 1 iteration, halo depth >= 2 and >= 16 "
+                                "interior rows per slab (rank " + std::to_string(m->rank) + " has " +
+                                    std::to_string(hi - lo) + ", halo depth " +
+                                    std::to_string(m->g.hg) + ")");
     return 0;
 }
 
@@ -1340,8 +1436,10 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         (rc = zalloc((void **)&m->ctl, sizeof(Ctl))) ||
         (rc = zalloc((void **)&m->slots, kSlotWords * 4)))
         return rc;
-    HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 4, hipHostMallocMapped | hipHostMallocCoherent));
+    // word 0: first non-finite step; word 1: last finished step (watchdog)
+    HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 8, hipHostMallocMapped | hipHostMallocCoherent));
     *(volatile uint32_t *)m->h_nonfinite = 0u;
+    *(volatile uint32_t *)(m->h_nonfinite + 1) = 0u;
     HIP_TRY(hipHostMalloc((void **)&m->h_res, 4 * cfd_model::kResRing, hipHostMallocDefault));
     for (hipEvent_t &e : m->ev_res) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char *to = getenv("CFD_RCCL_TIMEOUT_S")) m->rccl_timeout_s = std::max(1.0, atof(to));
@@ -1428,6 +1526,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         void *dp = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&dp, m->h_nonfinite, 0));
         f.host_nonfinite = (uint32_t *)dp;
+        f.host_progress = m->n_ranks > 1 ? (uint32_t *)dp + 1 : nullptr;
     }
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
@@ -1440,6 +1539,51 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     HIP_TRY(hipMemcpyAsync(m->ctl, &c0, sizeof(Ctl), hipMemcpyHostToDevice, m->stream));
     HIP_TRY(hipStreamSynchronize(m->stream));
     return 0;
+}
+
+// Communicator creation with a deadline: a non-blocking
+// ncclCommInitRankConfig, polled until every rank has joined or
+// CFD_RCCL_TIMEOUT_S passes (then aborted: CFD_ERCCL instead of hanging in
+// cfd_create_sharded when a peer never arrives).  CFD_RCCL_BLOCKING_INIT=1
+// restores the plain blocking ncclCommInitRank.
+int comm_init(cfd_model *m, const ncclUniqueId &id, int n_ranks, int rank) {
+    const char *blk = getenv("CFD_RCCL_BLOCKING_INIT");
+    if (blk && atoi(blk) == 1) {
+        const ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, id, rank);
+        if (r != ncclSuccess) {
+            m->comm = nullptr;
+            return fail(CFD_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+        return 0;
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&m->comm, n_ranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (m->comm) ncclCommAbort(m->comm);
+        m->comm = nullptr;
+        return fail(CFD_ERCCL, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclInProgress;
+        r = ncclCommGetAsyncError(m->comm, &st);
+        if (r == ncclSuccess) r = st;
+        if (r == ncclSuccess) return 0;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (r != ncclInProgress || el > m->rccl_timeout_s) {
+            ncclCommAbort(m->comm);
+            m->comm = nullptr;
+            return fail(CFD_ERCCL,
+                        r != ncclInProgress
+                            ? std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r)
+                            : "ncclCommInitRankConfig: rank " + std::to_string(rank) + " of " +
+                                  std::to_string(n_ranks) + ": not every rank joined within " +
+                                  std::to_string((int)m->rccl_timeout_s) +
+                                  " s (CFD_RCCL_TIMEOUT_S); the communicator was aborted");
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
 }
 
 int create_common(const cfd_grid *grid, const cfd_params *params, int device, int n_ranks, int rank,
@@ -1474,6 +1618,7 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
         }
     }
     rc = build_model(m, grid, params, device, hg);
+    if (!rc) rc = validate_sharded(m, params);
     if (!rc && n_ranks > 1 && hub) {
         if (hub->n != n_ranks) {
             rc = fail(CFD_EINVAL, "local hub size != n_ranks");
@@ -1485,8 +1630,7 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     } else if (!rc && n_ranks > 1) {
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
-        ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, id, rank);
-        if (r != ncclSuccess) rc = fail(CFD_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        rc = comm_init(m, id, n_ranks, rank);
     }
     if (rc) {
         m->destroy();
@@ -1513,7 +1657,7 @@ int cfdrt_check_params(const cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
     if (rc) return rc;
-    return 0;
+    return validate_sharded(m, p);
 }
 
 int cfd_get_config(const cfd_model *m, cfd_grid *grid, cfd_params *params) {
@@ -1585,6 +1729,33 @@ int cfd_create_sharded_local(const cfd_grid *grid, const cfd_params *params, int
     if (!hub) return fail(CFD_EINVAL, "null local hub");
     return create_common(grid, params, device_ordinal, n_ranks, rank, nullptr,
                          static_cast<LocalHub *>(hub), out);
+}
+
+int cfd_device_count(int *n_out) {
+    if (!n_out) return fail(CFD_EINVAL, "null out");
+    *n_out = 0;
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess && e != hipErrorNoDevice)
+        return fail(CFD_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *n_out = e == hipSuccess ? n : 0;
+    return 0;
+}
+
+int cfd_get_comm_size(const cfd_model *m, int *n_out) {
+    if (!m || !n_out) return fail(CFD_EINVAL, "null model or out");
+    if (m->hub) {
+        *n_out = m->hub->n;
+    } else if (m->comm) {
+        int n = 0;
+        RCCL_TRY(ncclCommCount(m->comm, &n));
+        *n_out = n;
+    } else if (m->n_ranks > 1) {
+        return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+    } else {
+        *n_out = 1;
+    }
+    return 0;
 }
 
 int cfd_get_slab(const cfd_model *m, uint64_t *j0, uint64_t *j1) {
@@ -1677,6 +1848,8 @@ int cfd_run_phase(cfd_model *m, int phase, float dt_sub) {
 int cfd_set_params(cfd_model *m, const cfd_params *p) {
     if (!m) return fail(CFD_EINVAL, "null model");
     int rc = validate(&m->grid, p);
+    if (rc) return rc;
+    rc = validate_sharded(m, p);
     if (rc) return rc;
     rc = m->sync();
     if (rc) return rc;
@@ -1894,6 +2067,8 @@ int cfd_timing_begin(cfd_model *m) {
     m->ev_next = 0;
     m->solve_events.clear();
     m->step_events.clear();
+    m->phase_events[0].clear();
+    m->phase_events[1].clear();
     m->timed_sweeps = 0;
     m->timed_launches = 0;
     m->timed_steps = 0;
@@ -1915,6 +2090,16 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
         HIP_TRY(hipEventElapsedTime(&ms, m->step_events[k], m->step_events[k + 1]));
         t_ms += ms;
     }
+    for (int ph = 0; ph < 2; ++ph) {
+        m->phase_ms[ph] = 0.0;
+        for (auto &pr : m->phase_events[ph]) {
+            float ms = 0.f;
+            if (!pr.second) continue;
+            HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+            m->phase_ms[ph] += ms;
+        }
+        m->phase_events[ph].clear();
+    }
     if (solve_ms) *solve_ms = s_ms;
     if (sweeps) *sweeps = m->timed_sweeps;
     if (step_ms) *step_ms = t_ms;
@@ -1923,6 +2108,19 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
     m->ev_next = 0;
     m->solve_events.clear();
     m->step_events.clear();
+    return 0;
+}
+
+int cfd_timing_phases(cfd_model *m, int on) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    m->timing_phases = on != 0;
+    return 0;
+}
+
+int cfd_timing_phase_ms(const cfd_model *m, double *predict_ms, double *finish_ms) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (predict_ms) *predict_ms = m->phase_ms[0];
+    if (finish_ms) *finish_ms = m->phase_ms[1];
     return 0;
 }
 

@@ -671,7 +671,13 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5m(MgLevel L, const float *
     const int gxc = min(max(gx, 0), nx - 1);
     const float *__restrict__ ps = src + gxc;
     const float *__restrict__ prh = L.rhs + gxc;
+    // the warm-up slots read ring rows from before slot 0; their values reach
+    // only rows that are never stored, but they must not be uninitialised
     float W[NS][4];
+#pragma unroll
+    for (int a = 0; a < NS; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) W[a][b] = 0.0f;
     float RH[kMgU];
     float PQ[4];
     ProlongIn EQ[4];

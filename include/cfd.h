@@ -142,6 +142,12 @@ void *cfd_local_hub_create(int n_ranks);
 void cfd_local_hub_destroy(void *hub);
 int cfd_create_sharded_local(const cfd_grid *grid, const cfd_params *params, int device_ordinal,
                              int n_ranks, int rank, void *hub, cfd_model **out);
+/* HIP devices visible to this process (bench.py's launched ranks check that
+ * there is one per rank before creating anything). */
+int cfd_device_count(int *n_out);
+/* Ranks the model's transport reports: ncclCommCount of the RCCL
+ * communicator, the LocalHub's size, or 1 for an unsharded model. */
+int cfd_get_comm_size(const cfd_model *m, int *n_out);
 /* Global pressure rows [j0, j1) held by this model (0, ny for cfd_create). */
 int cfd_get_slab(const cfd_model *m, uint64_t *j0, uint64_t *j1);
 
@@ -191,6 +197,14 @@ int cfd_profile_sweeps(cfd_model *m, int n_sweeps, double *avg_ms_out);
 int cfd_timing_begin(cfd_model *m);
 int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *step_ms,
                    uint64_t *steps);
+/* Per-phase timing inside the timing window (off by default: every event
+ * record costs the step a few microseconds): with on != 0, the following
+ * cfd_timing_begin/end windows also time each step's predictor + first
+ * divergence phase (model.rs:538-676) and its corrector / fused finish
+ * (model.rs:693, 728, 333-377); cfd_timing_phase_ms returns the sums of the
+ * last window (0 when a phase was not timed). */
+int cfd_timing_phases(cfd_model *m, int on);
+int cfd_timing_phase_ms(const cfd_model *m, double *predict_ms, double *finish_ms);
 /* p' halo depth (rows exchanged per RCCL round) of a sharded model. */
 int cfd_get_halo_depth(const cfd_model *m);
 /* Jacobi kernel configuration chosen at creation: division form proven exact

@@ -256,3 +256,109 @@ def test_sharded_multigrid_matches_oracle(monkeypatch, n, tol, smooth):
     st = run_sharded(n, grid, params, 4, 4)
     check_against_oracle(st, grid, dict(pressure_solver=2, corrector_passes=3,
                                         tol_enabled=int(tol)), 4, FIELDS + ("rhs",))
+
+
+def _slab_slices(st, nx, j0, j1):
+    out = {}
+    for k in ("u", "u_star"):
+        out[k] = st[k].reshape(-1, nx + 1)[j0:j1].ravel().copy()
+    for k in ("v", "v_star"):
+        out[k] = st[k].reshape(-1, nx)[j0:j1 + 1].ravel().copy()
+    for k in ("p", "p_prime", "rhs"):
+        out[k] = st[k].reshape(-1, nx)[j0:j1].ravel().copy()
+    for k in ("dt", "simulation_time", "simulation_step", "last_p_residual", "last_u_residual",
+              "last_v_residual", "jacobi_sweeps_total"):
+        out[k] = st[k]
+    return out
+
+
+def run_sharded_from_state(n, grid, params, state, steps):
+    """LocalHub slabs started from a single-domain state (cfd_set_state on
+    every slab, collective: it exchanges the ghosts)."""
+    import cfdamd
+    hub = cfdamd.LocalHub(n)
+    states, models, errors = [None] * n, [None] * n, []
+
+    def worker(r):
+        try:
+            m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=r, local_hub=hub)
+            models[r] = m
+            m.set_state(**_slab_slices(state, grid.nx, m.j0, m.j1))
+            m.update_n(steps)
+            m.synchronize()
+            states[r] = (m.j0, m.j1, m.get_state(), m.halo_depth)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(900)
+    for m in models:
+        if m is not None:
+            m.close()
+    hub.close()
+    if errors:
+        raise errors[0]
+    return states
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n,nx,ny", [(2, 8192, 4096), (8, 16384, 8192)])
+def test_sharded_full_size_developed_across_boundaries(n, nx, ny):
+    """C4 (2 slabs of 8192x2048) and C5 (8 slabs of 16384x1024) at bench.py's
+    default halo depth (32) from a DEVELOPED cavity: the single-domain model
+    runs 400 timed-mode steps, its state is injected into the slabs, and two
+    more steps on the slabs equal two more single-domain steps bit for bit.
+    Unlike 4 steps from rest, the rows either side of every slab boundary
+    now carry developed p' (>= 90 % non-zero), so the deep-halo exchange,
+    the overlapped bands and the rhs/u/v ghosts move real data.  For C4 one
+    step is also checked against the oracle from the developed state."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(nx, ny)
+    params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
+    m = cfdamd.Model(grid, params, device=0)
+    try:
+        m.update_n(400)
+        st0 = m.get_state()
+        m.update_n(2)
+        ref = m.get_state()
+    finally:
+        m.close()
+    pp = st0["p_prime"].reshape(ny, nx)
+    import ctypes as C
+    L = cfdamd.load()
+    j0, j1 = C.c_uint64(), C.c_uint64()
+    bounds = []
+    for r in range(1, n):
+        L.cfd_plan_slab(ny, n, r, C.byref(j0), C.byref(j1))
+        bounds.append(int(j0.value))
+    rows = sorted({b + d for b in bounds for d in (-1, 0)})
+    frac = np.count_nonzero(pp[rows]) / float(len(rows) * nx)
+    assert frac >= 0.9, f"boundary rows {rows}: only {frac:.3f} of p' non-zero"
+    st = run_sharded_from_state(n, grid, params, st0, 2)
+    assert all(s[3] == 32 for s in st), [s[3] for s in st]
+    got = assemble(st, nx)
+    del st
+    for f in FIELDS + ("rhs",):
+        assert_bitwise(f"{f} ({n} slabs, developed, vs single domain {nx}x{ny})", got[f], ref[f])
+    del got, ref
+    if n == 2:
+        from oracle import OracleModel
+        import oracle as orc
+        orc.set_threads(min(16, os.cpu_count() or 1))
+        o = OracleModel(nx, ny, float(nx) / ny, 1.0, bc_kind=1, viscosity=0.001,
+                        jacobi_iters=200, corrector_passes=0, tol_enabled=0)
+        for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
+            o.field(k)[:] = st0[k]
+        sc = o.scalars()
+        sc.step, sc.time, sc.dt = st0["simulation_step"], st0["simulation_time"], st0["dt"]
+        sc.jacobi_sweeps_total = st0["jacobi_sweeps_total"]
+        o.set_scalars(sc)
+        o.update()
+        orc.set_threads(1)
+        one = run_sharded_from_state(n, grid, params, st0, 1)
+        got1 = assemble(one, nx)
+        for f in FIELDS + ("rhs",):
+            assert_bitwise(f"{f} (2 slabs, 1 developed step) vs oracle", got1[f], o.field(f))

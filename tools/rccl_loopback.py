@@ -58,6 +58,9 @@ def worker(args):
                               cfdamd.Grid(args.nx, args.ny, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5)),
                               cfdamd.SimulationParams(pressure_solver=solver, jacobi_iters=40,
                                                       corrector_passes=2, tol_enabled=tol)))
+    if args.mode == "developed":
+        developed(args, rank, n, cfdamd, dist, np)
+        return
     report = []
     for name, grid, params in cases:
         if rank == 0:
@@ -108,13 +111,80 @@ def worker(args):
     dist.destroy_process_group()
 
 
+def slab_slices(st, nx, j0, j1):
+    """Rows [j0, j1) of a single-domain state (v and v* with face row j1)."""
+    out = {}
+    for k in ("u", "u_star"):
+        out[k] = st[k].reshape(-1, nx + 1)[j0:j1].ravel().copy()
+    for k in ("v", "v_star"):
+        out[k] = st[k].reshape(-1, nx)[j0:j1 + 1].ravel().copy()
+    for k in ("p", "p_prime", "rhs"):
+        out[k] = st[k].reshape(-1, nx)[j0:j1].ravel().copy()
+    for k in ("dt", "simulation_time", "simulation_step", "last_p_residual", "last_u_residual",
+              "last_v_residual", "jacobi_sweeps_total"):
+        out[k] = st[k]
+    return out
+
+
+def developed(args, rank, n, cfdamd, dist, np):
+    """The bench's timed mode on a DEVELOPED cavity: every rank develops the
+    single-domain model for --develop steps (deterministic, so every rank
+    holds the same bits), injects its slab rows into the RCCL-sharded model
+    (cfd_set_state exchanges the ghosts), and runs --steps steps; its rows
+    must equal the single-domain continuation bit for bit.  The slab
+    boundaries carry developed p' (the non-zero fraction of the rows either
+    side of each boundary is reported)."""
+    grid = cfdamd.cavity_grid(args.nx, args.ny)
+    params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
+    nx = args.nx
+    ref = cfdamd.Model(grid, params, device=0)
+    ref.update_n(args.develop)
+    st0 = ref.get_state()
+    ref.update_n(args.steps)
+    want = ref.get_state()
+    ref.close()
+    obj = [cfdamd.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    t0 = time.perf_counter()
+    m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=rank, unique_id=obj[0])
+    j0, j1 = m.j0, m.j1
+    m.set_state(**slab_slices(st0, nx, j0, j1))
+    m.update_n(args.steps)
+    m.synchronize()
+    el = time.perf_counter() - t0
+    got = m.get_state()
+    ranks_seen = m.comm_size
+    m.close()
+    exp = slab_slices(want, nx, j0, j1)
+    bad = [k for k in ("u", "v", "p", "p_prime", "u_star", "v_star", "rhs")
+           if not np.array_equal(got[k].view(np.uint32), exp[k].view(np.uint32))]
+    pp = st0["p_prime"].reshape(-1, nx)
+    # the p' rows either side of this slab's internal boundaries
+    rows = ([j0 - 1, j0] if j0 > 0 else []) + ([j1 - 1, j1] if j1 < args.ny else [])
+    nzf = float(np.count_nonzero(pp[rows])) / max(len(rows) * nx, 1) if rows else None
+    print(json.dumps({"case": "developed cavity, fixed-count (deep halos, overlapped exchange)",
+                      "rank": rank, "ranks": n, "ranks_seen": ranks_seen,
+                      "grid": [args.nx, args.ny], "slab": [j0, j1], "develop": args.develop,
+                      "steps": args.steps, "boundary_rows": rows,
+                      "boundary_pprime_nonzero_frac": nzf,
+                      "bitwise_equal_single_domain": not bad, "differ": bad,
+                      "sharded_wall_s": round(el, 3)}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    if bad:
+        sys.exit(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=2)
     ap.add_argument("--nx", type=int, default=256)
     ap.add_argument("--ny", type=int, default=200)
     ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--mode", default="both", choices=["fixed", "tol", "both", "solvers"])
+    ap.add_argument("--mode", default="both",
+                    choices=["fixed", "tol", "both", "solvers", "developed"])
+    ap.add_argument("--develop", type=int, default=400)
+    ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
@@ -130,12 +200,12 @@ def main():
                    MASTER_PORT=str(port), LOCAL_RANK="0")
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--n", str(args.n),
                "--nx", str(args.nx), "--ny", str(args.ny), "--steps", str(args.steps),
-               "--mode", args.mode]
+               "--mode", args.mode, "--develop", str(args.develop)]
         procs.append(subprocess.Popen(cmd, env=env))
     rc = 0
     for p in procs:
         try:
-            rc |= p.wait(timeout=240)
+            rc |= p.wait(timeout=args.timeout)
         except subprocess.TimeoutExpired:
             p.kill()
             rc |= 1
