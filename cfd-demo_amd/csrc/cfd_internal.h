@@ -57,6 +57,12 @@ struct Ctl {
     uint32_t vis[2];        // render: max key, max ~key of the derived field (cfd_render.hip)
     uint32_t done;          // workgroups finished (last-workgroup folds); 0 between launches
     uint64_t sweeps_total;
+    // speculative temporal blocking with the tolerance on (k_spec_check):
+    // spec_stop: a launch of this solve converged (later launches skip);
+    // spec_launch / spec_redo: that launch and the stages its re-run keeps
+    // (0: none, it converged on its last stage); spec_launches: launches run
+    // (the finalize's buffer flips).  All 0 between solves.
+    int32_t spec_stop, spec_redo, spec_launch, spec_launches;
     int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
     uint32_t err[kMaxSweeps];        // per-sweep max |p'new - p'| as f32 bits
 };
@@ -164,9 +170,22 @@ void launch_pipe4(const Geom &g, const Fields &f, int T, int pass, int it, int p
                   int out_hi, uint32_t *res_slots, hipStream_t s);
 void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
                   int out_hi, uint32_t *res_slots, hipStream_t s);
-// kind 5: the same march with its rhs window in LDS (cfd_jacobi_lds.hip, T <= 8)
+// kind 5: the same march with its rhs window in LDS (cfd_jacobi_lds.hip, T <= 8);
+// mode 2 / 3: the speculative launch / its re-run (launch_jacobi_spec)
 void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                int out_hi, uint32_t *res_slots, hipStream_t s);
+                int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0);
+// Speculative temporal blocking for the tolerance mode (model.rs:748-819):
+// the launch starting at sweep `it` runs T sweeps (kind 5) and publishes
+// every sweep's residual; k_spec_check folds them, finds the first sweep
+// below p_tol and, when it is not the launch's last, schedules the re-run
+// (launch_jacobi_redo) of that launch with exactly that many sweeps from its
+// untouched source buffer.  Later launches of the solve return at once.
+void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,
+                        int out_lo, int out_hi, hipStream_t s);
+void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, int par,
+                       hipStream_t s);
+void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
+                        hipStream_t s);
 // dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before
 // an all-reduce of dst reads it).
 void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s);
@@ -184,7 +203,8 @@ void launch_verify_division(float c, float r, unsigned long long *dev_counts, hi
 // flips = launches of a fixed-count solve (ignored with the tolerance on,
 // where each executed sweep is one launch).  exact_flips: flip the current
 // p' buffer exactly `flips` times regardless of the tolerance (solvers that
-// work in place: SOR, multigrid).
+// work in place: SOR, multigrid); 2: Ctl::spec_launches times (speculative
+// solve), and reset the speculative state.
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
                            int flips, hipStream_t s, int exact_flips = 0);
 

@@ -84,8 +84,15 @@ constexpr int ring_depth(int T, int PD, int L) {
     return ((L * T + 1 + q - 1) / q) * q;
 }
 
-template <int T, int FAST, bool RES>
+// MODE: 0 plain launch; 1 (RES) the solve's last launch, publishes the last
+// stage's residual; 2 (SPEC) the speculative tolerance-mode launch: every
+// stage's residual goes to its own sweep's slot set, and the launch is skipped
+// once an earlier launch of the solve converged (Ctl::spec_stop); 3 (REDO)
+// re-runs the converged launch from its untouched source buffer with the
+// run-time stage count Ctl::spec_redo < T (stores only the segment's rows).
+template <int T, int FAST, int MODE>
 struct LdsMarch {
+    static constexpr bool RES = MODE == 1, SPEC = MODE == 2, REDO = MODE == 3;
     // Lag L: stage s of slot v computes row k - L*s.  L = 1 is the plain
     // pipeline (stage s reads stage s-1's row of the SAME slot: one serial
     // chain of T updates per slot).  L = 2 skews the stages so that stage s
@@ -107,7 +114,10 @@ struct LdsMarch {
     f2 W[T][NW];
     f2 PQ[PD];
     f2 RQ[PD];
-    float2 *ring;        // this wave's D x 64 slots (LDS)
+    // this wave's D x 64 slots (LDS).  Typed as the packed pair itself: a
+    // float2-struct ring made the compiler split every read into a b32 and a
+    // b64 load plus a v_mov per stage
+    f2 *ring;
     int lane;
     int k_first, S, lo_clamp, hi_clamp, nch, g_first, g_last, g_top, g_zero, row_bytes;
     int ch, vo_ld, vo_st, abase, dir;
@@ -115,6 +125,9 @@ struct LdsMarch {
     const Geom *g;       // the kernel argument: divisors and their reciprocals
     __amdgpu_buffer_rsrc_t rs_p, rs_r, rs_d;
     float m;
+    float mm[SPEC ? T : 1];   // SPEC: stage s's residual (segment rows only)
+    int r0v, r1v;             // the segment's output rows (march order)
+    int nst;                  // REDO: stages to run (< T)
 
     __device__ __forceinline__ int act(int vrow) const { return abase + dir * vrow; }
 
@@ -178,12 +191,12 @@ struct LdsMarch {
         W[0][V_ % NW] = PQ[V_ % PD];                                 // input row k
         PQ[V_ % PD] = ld(rs_p, k + PD);
         if (!(CFD_LDS_DIAG & 2))
-            ring[(V_ % D) * 64 + lane] = make_float2(RQ[V_ % PD].x, RQ[V_ % PD].y);   // rhs row k
+            ring[(V_ % D) * 64 + lane] = RQ[V_ % PD];                 // rhs row k
         RQ[V_ % PD] = ld(rs_r, k + PD);
         // the slot's T ring reads issued together (the ring rows of earlier
         // slots; this slot's write went to another entry): one LDS latency
         // per slot instead of one per stage
-        float2 rhv[T];
+        f2 rhv[T];
         if (CFD_LDS_HOIST && !(CFD_LDS_DIAG & 2)) {
 #pragma unroll
             for (int s = 1; s <= T; ++s) rhv[s - 1] = ring[((V_ - L * s + 8 * D) % D) * 64 + lane];
@@ -194,17 +207,40 @@ struct LdsMarch {
             if (GUARD == 3 && v < (L + 1) * s) continue;             // wave-uniform
             if (CFD_LDS_SB >= 2 && s > 1) __builtin_amdgcn_sched_barrier(0);
             const int r = k - L * s;
-            const float2 rh = (CFD_LDS_DIAG & 2)
-                                  ? make_float2(RQ[(V_ + s) % PD].x, RQ[(V_ + s) % PD].y)
-                                  : (CFD_LDS_HOIST ? rhv[s - 1]
-                                                   : ring[((V_ - L * s + 8 * D) % D) * 64 + lane]);
+            const f2 rh = (CFD_LDS_DIAG & 2) ? RQ[(V_ + s) % PD]
+                                             : (CFD_LDS_HOIST ? rhv[s - 1]
+                                                              : ring[((V_ - L * s + 8 * D) % D) * 64 + lane]);
             // stage s-1 finished row x at slot x - k_first + L(s-1)
             constexpr int kW = 4 * NW;
             const f2 &B = W[s - 1][(V_ - L - 1 + kW) % NW];          // stage s-1, row r-1
             const f2 &C = W[s - 1][(V_ - L + kW) % NW];              //            row r
             const f2 &Tp = W[s - 1][(V_ + 1 - L + kW) % NW];         //            row r+1
-            f2 n = stage<E>(B, C, Tp, (f2){rh.x, rh.y});
-            if (s < T) {
+            if (REDO && s > nst) continue;                            // wave-uniform
+            f2 n = stage<E>(B, C, Tp, rh);
+            if (SPEC && r >= r0v && r < r1v) {
+                // every stage is one reference sweep: its max |new - old| over
+                // the segment's own rows (each row counted by one segment)
+                const int ra = act(r);
+                if (ra >= 0 && ra < nyl_) {
+                    const f2 d = n - C;
+                    if (!(E & kCol)) {
+                        mm[s - 1] = fmaxf(fmaxf(mm[s - 1], fabsf(d.x)), fabsf(d.y));
+                    } else {
+                        if (e0) mm[s - 1] = fmaxf(mm[s - 1], fabsf(d.x));
+                        if (e1) mm[s - 1] = fmaxf(mm[s - 1], fabsf(d.y));
+                    }
+                }
+            }
+            if (REDO && s == nst) {
+                // the stored stage: only rows of this segment (the march
+                // computes the T-stage window, wider than nst stages need)
+                if (r >= r0v && r < r1v) {
+                    const int ra = act(r);
+                    st(n, ra);
+                    if ((E & kRow) && r == g_first) st(n, g_zero);
+                    if ((E & kRow) && r == g_last) st(n, g_top);
+                }
+            } else if (s < T) {
                 // stage s's row r-1 is its previous slot's row
                 if ((E & kRow) && r == g_top) n = W[s][(V_ - 1 + kW) % NW]; // P(i,ny-1) = P(i,ny-2)
                 W[s][V_ % NW] = n;
@@ -305,13 +341,14 @@ struct LdsMarch {
 #else
 #define CFD_LDS_BOUNDS __launch_bounds__(kLdsWaves * 64)
 #endif
-template <int T, int FAST, bool RES>
+template <int T, int FAST, int MODE>
 __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
     int wlo, int whi) {
-    using M = LdsMarch<T, FAST, RES>;
-    __shared__ float2 lds[kLdsWaves * M::D * 64];
+    using M = LdsMarch<T, FAST, MODE>;
+    constexpr bool RES = M::RES;
+    __shared__ f2 lds[kLdsWaves * M::D * 64];
 #if CFD_LDS_STAMP
     const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
@@ -335,7 +372,13 @@ __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
     } stamp_guard{st_rt0, st_t0};
 #endif
     if (pass_off(ctl, pass)) return;
+    if (M::SPEC && ctl->spec_stop) return;   // an earlier launch of the solve converged
     M w;
+    if (M::REDO) {
+        w.nst = ctl->spec_redo;
+        if (w.nst <= 0) return;
+        par = ctl->spec_launch;   // re-run that launch: same source, same destination
+    }
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int lane = (int)threadIdx.x & 63;
     const int bid = xcd_block(g);
@@ -383,6 +426,10 @@ __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
     w.g_top = g.ny - 1 - g.j0;
     w.g_zero = -g.j0;
     w.m = 0.0f;
+#pragma unroll
+    for (int s = 0; s < (M::SPEC ? T : 1); ++s) w.mm[s] = 0.0f;
+    w.r0v = r0;
+    w.r1v = r1;
     w.k_first = r0 - T;
     w.S = (r1 - r0) + M::WARM;
     w.abase = 0;
@@ -419,6 +466,14 @@ __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
         w.template run<M::kCol>();
     else
         w.template run<0>();
+    if (M::SPEC) {
+#pragma unroll
+        for (int s = 0; s < T; ++s) {
+            const float ms = wave_max(out_lane ? w.mm[s] : 0.0f);
+            if (lane == 0)
+                publish_max(res_slots + (size_t)s * kResSlots * kResStride, bid * kLdsWaves + wave, ms);
+        }
+    }
     if (!RES) return;
     const float m = wave_max(out_lane ? w.m : 0.0f);
     if (lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, m);
@@ -426,12 +481,12 @@ __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
 
 // Workgroups of k_jacobi_lds<T, FAST, RES> one CU holds at once (occupancy
 // API, cached per instantiation).
-template <int T, int FAST, bool RES>
+template <int T, int FAST, int MODE>
 int lds_blocks_per_cu() {
     static const int nb = [] {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &n, reinterpret_cast<const void *>(&k_jacobi_lds<T, FAST, RES>), kLdsWaves * 64, 0) !=
+                &n, reinterpret_cast<const void *>(&k_jacobi_lds<T, FAST, MODE>), kLdsWaves * 64, 0) !=
                 hipSuccess ||
             n < 1)
             n = 1;
@@ -445,25 +500,25 @@ int lds_blocks_per_cu() {
 // SIMD gets its waves at once and the same march length, so no CU waits for a
 // second, partial round — or whole multiples of a round when a round would
 // make segments longer than kMaxRows.
-template <int T, int FAST, bool RES>
+template <int T, int FAST, int MODE>
 int lds_segments(const Geom &g, int nrows, int nwc) {
     if (g.tb_rows > 0) return cdiv(nrows, g.tb_rows);
     constexpr int kMaxRows = 160, kMinRows = 8;
-    const int wgs_per_col = std::max(1, g.n_cu * lds_blocks_per_cu<T, FAST, RES>() / nwc);
+    const int wgs_per_col = std::max(1, g.n_cu * lds_blocks_per_cu<T, FAST, MODE>() / nwc);
     const int per_round = kLdsWaves * wgs_per_col;
     const int rounds = std::max(1, cdiv(nrows, (long)per_round * kMaxRows));
     return std::max(1, std::min(per_round * rounds, nrows / kMinRows));
 }
 
-template <int T, bool RES>
+template <int T, int MODE>
 void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
                   uint32_t *rs, hipStream_t s) {
     const int nch = g.nx / 2;
-    const int nwc = cdiv(nch, LdsMarch<T, 1, RES>::OUTL);
+    const int nwc = cdiv(nch, LdsMarch<T, 1, MODE>::OUTL);
     const int nrows = out_hi - out_lo;
-    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, RES>(g, nrows, nwc)
-                     : g.fastdiv == 2 ? lds_segments<T, 2, RES>(g, nrows, nwc)
-                                      : lds_segments<T, 0, RES>(g, nrows, nwc);
+    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, MODE>(g, nrows, nwc)
+                     : g.fastdiv == 2 ? lds_segments<T, 2, MODE>(g, nrows, nwc)
+                                      : lds_segments<T, 0, MODE>(g, nrows, nwc);
     const dim3 grid(nwc * cdiv(nseg, kLdsWaves)), block(kLdsWaves * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     // a segment whose rows reach a global boundary row runs the kCol|kRow
@@ -474,7 +529,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo,
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
-    hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, RES>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, \
+    hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, \
                        rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);
@@ -485,22 +540,33 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo,
 #undef CFD_LDS_LAUNCH
 }
 
-// T sweeps per launch, with (rs != nullptr) or without the residual.
+// T sweeps per launch: mode 0 / 1 (plain / last-stage residual, chosen by
+// rs != nullptr), 2 (SPEC, rs = the first stage's slot set), 3 (REDO, T = 8).
 template <int T>
 void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
-                  uint32_t *rs, hipStream_t s) {
+                  uint32_t *rs, int mode, hipStream_t s) {
+    if (mode == 2) {
+        launch_lds_t<T, 2>(g, f, pass, par, out_lo, out_hi, rs, s);
+        return;
+    }
+    if constexpr (T == 8) {
+        if (mode == 3) {
+            launch_lds_t<8, 3>(g, f, pass, par, out_lo, out_hi, rs, s);
+            return;
+        }
+    }
     if (rs)
-        launch_lds_t<T, true>(g, f, pass, par, out_lo, out_hi, rs, s);
+        launch_lds_t<T, 1>(g, f, pass, par, out_lo, out_hi, rs, s);
     else
-        launch_lds_t<T, false>(g, f, pass, par, out_lo, out_hi, rs, s);
+        launch_lds_t<T, 0>(g, f, pass, par, out_lo, out_hi, rs, s);
 }
 
 }  // namespace
 
 // per-translation-unit entry points (cfd_jacobi_lds*.hip)
 void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int out_lo,
-                     int out_hi, uint32_t *rs, hipStream_t s);
+                     int out_hi, uint32_t *rs, int mode, hipStream_t s);
 void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
-                   uint32_t *rs, hipStream_t s);
+                   uint32_t *rs, int mode, hipStream_t s);
 
 }  // namespace cfd

@@ -5,8 +5,8 @@
 namespace cfd {
 
 void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
-                   uint32_t *rs, hipStream_t s) {
-    launch_lds_T<8>(g, f, pass, par, out_lo, out_hi, rs, s);
+                   uint32_t *rs, int mode, hipStream_t s) {
+    launch_lds_T<8>(g, f, pass, par, out_lo, out_hi, rs, mode, s);
 }
 
 #if CFD_LDS_STAMP

@@ -664,7 +664,8 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
             const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
             // one buffer flip per launch: per sweep with the tolerance on,
             // `flips` (host-known launch count) for fixed-count solves
-            c->cur = (c->cur + ((g.tol_enabled && !exact_flips) ? n : flips)) & 1;
+            c->cur = (c->cur + (exact_flips == 2 ? c->spec_launches
+                                : (g.tol_enabled && !exact_flips) ? n : flips)) & 1;
             c->last_p = res;
             c->red[5] = __float_as_uint(res);   // the step-end all-reduce carries it (slabs)
             c->n_exec_last = (uint32_t)n;
@@ -672,6 +673,7 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
         }
         if (pass >= 0 && pass + 1 <= kMaxPasses)
             c->go[pass + 1] = (go && !(check_break && g.tol_enabled && c->last_p < g.p_tol)) ? 1 : 0;
+        if (exact_flips == 2) c->spec_stop = c->spec_redo = c->spec_launch = c->spec_launches = 0;
         go_s = go;
     }
     __syncthreads();
@@ -683,6 +685,34 @@ __global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int
                                                            int check_break, int flips,
                                                            int exact_flips) {
     solve_finalize_body(g, f, pass, iters, check_break, flips, exact_flips);
+}
+
+// After the speculative launch covering sweeps [it, it+T) (launch_jacobi_spec):
+// fold its T residual slot sets into Ctl::err, and find the first of its
+// sweeps whose residual is below p_tol (model.rs:816).  That sweep ends the
+// solve: later launches skip (spec_stop), and unless it is the launch's last
+// sweep the launch is re-run with exactly that many sweeps (spec_redo).
+__global__ __launch_bounds__(kBlock) void k_spec_check(Geom g, Fields f, int pass, int it, int T,
+                                                       int par) {
+    Ctl *c = f.ctl;
+    if (pass_off(c, pass) || c->spec_stop) return;
+    const int wv = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+    for (int k = it + wv; k < it + T; k += nw) {
+        uint32_t *set = f.err_slots + (size_t)k * kResSlots * kResStride;
+        const float v = read_max(set, c->err[k]);
+        if ((threadIdx.x & 63) < kResSlots) set[(threadIdx.x & 63) * kResStride] = 0u;
+        if ((threadIdx.x & 63) == 0) c->err[k] = __float_as_uint(v);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int j = 0;
+    while (j < T && !(__uint_as_float(c->err[it + j]) < g.p_tol)) ++j;
+    c->spec_launches = par + 1;
+    if (j < T) {
+        c->spec_stop = 1;
+        c->spec_launch = par;
+        c->spec_redo = j + 1 < T ? j + 1 : 0;
+    }
 }
 
 // dst[q] = max(dst[q], slots of set q), then zero the slots (q < n).
@@ -1386,6 +1416,24 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
         launch_lds(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else
         launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
+}
+
+void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,
+                        int out_lo, int out_hi, hipStream_t s) {
+    if (out_hi <= out_lo) return;
+    launch_lds(g, f, T, pass, it, par, out_lo, out_hi,
+               f.err_slots + (size_t)it * kResSlots * kResStride, s, 2);
+}
+
+void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, int par,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_check, dim3(1), dim3(kBlock), 0, s, g, f, pass, it, T, par);
+}
+
+void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
+                        hipStream_t s) {
+    if (out_hi <= out_lo) return;
+    launch_lds(g, f, kMaxTemporal, pass, 0, 0, out_lo, out_hi, nullptr, s, 3);
 }
 
 void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s) {

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <cstdio>
@@ -50,10 +51,9 @@ int fail(int code, const std::string &msg) {
             return fail(CFD_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(r_));    \
     } while (0)
 
-// An operation on the model's communicator.  The communicator is created
-// non-blocking (so its creation can time out, create_common), which lets any
-// call on it return ncclInProgress: settle() then waits, under the RCCL
-// deadline, until the communicator's state leaves ncclInProgress.
+// An operation on the model's communicator.  Should a call return
+// ncclInProgress (a non-blocking communicator), settle() waits, under the
+// RCCL deadline, until the communicator's state leaves ncclInProgress.
 #define RCCL_OP(expr)                                                                      \
     do {                                                                                   \
         int rc_ = settle((expr), #expr);                                                   \
@@ -441,6 +441,7 @@ struct cfd_model {
         const bool tol = g.tol_enabled != 0;
         float res_local = 0.f;
         if (tol && !residual_out) residual_out = &res_local;
+        if (!tol) return enqueue_sor_sharded_deep(k, pass, e0);
         int rc = exchange(FLD_RHS, HALO_PP, 1);
         if (rc) return rc;
         int n = iters, checked = 0;
@@ -505,6 +506,55 @@ struct cfd_model {
             if (rc) return rc;
             *residual_out = r;
         }
+        return 0;
+    }
+
+    // Fixed-count SOR on a slab with deep ghosts: an iteration's output rows
+    // [a, b) read p' rows [a-2, b+2) and rhs rows [a-1, b+1), so after an
+    // exchange of hg p' rows (and hg rhs rows once per solve) the next
+    // K = hg/2 iterations can each recompute a band of ghost rows two rows
+    // narrower than the one before, and p' crosses the link once every K
+    // iterations instead of after every one.  Iteration 0 reads no p' (the
+    // solve starts from 0).  Every ghost row is computed from the same values
+    // as its owner computes it, so the result is bitwise the single domain's.
+    int enqueue_sor_sharded_deep(const SorConst &k, int pass, hipEvent_t e0) {
+        const int iters = params.jacobi_iters;
+        const int glo = 1 - (int)j0, ghi = (int)g.ny - 1 - (int)j0;   // global rows 1..ny-2
+        const int K = std::max(1, g.hg / 2);
+        int rc = exchange(FLD_RHS, HALO_PP, g.hg);
+        if (rc) return rc;
+        for (int it = 0; it < iters; ++it) {
+            const int d = it % K;
+            const int a = std::max(glo, -g.hg + 2 * (d + 1));
+            const int b = std::min(ghi, g.nyl + g.hg - 2 * (d + 1));
+            const int res = it == iters - 1;
+            launch_sor_fused(f.pp[0], f.pp[1], f.rhs, g.nx, g.ny, k, f.ctl, f.err_slots, pass, it,
+                             0, g.p_tol, res, a, b, (int)j0, -g.hg, g.nyl + g.hg - 1, stream);
+            if (res) {
+                launch_fold_slots(f.ctl->err + it, f.err_slots + (size_t)it * kResSlots * kResStride,
+                                  1, stream);
+                rc = allreduce_max_u32(f.ctl->err + it, 1);
+                if (rc) return rc;
+            }
+            if (d == K - 1 && it + 1 < iters) {
+                rc = exchange_pp((host_cur + it + 1) & 1, g.hg);
+                if (rc) return rc;
+            }
+        }
+        // the corrector reads p' ghost rows -1 and nyl (the shared v faces):
+        // a last iteration that recomputed no ghost row (d == K-1) is
+        // followed by a full exchange; otherwise its recomputed band covers
+        // both, and only the deeper ghosts are stale
+        const bool last_bare = iters > 0 && (iters - 1) % K == K - 1;
+        if (last_bare) {
+            rc = exchange_pp((host_cur + iters) & 1, g.hg);
+            if (rc) return rc;
+        }
+        end_solve_timing(e0, (uint64_t)iters, (uint64_t)iters);
+        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, iters, stream);
+        HIP_TRY(hipGetLastError());
+        host_cur = (host_cur + iters) & 1;
+        pp_ghosts_shallow = !last_bare;
         return 0;
     }
 
@@ -745,10 +795,25 @@ struct cfd_model {
             e1 = take_event();
             HIP_TRY(hipEventRecord(e0, stream));
         }
+        const bool spec = spec_mode();
         const int tmax = g.tol_enabled ? 1 : t_max;
         int launches = 0;   // buffers flip once per launch
         if (!sharded()) {
-            if (tmax <= 1) {
+            if (spec) {
+                // the tolerance mode, temporally blocked (speculative): each
+                // launch runs kSpecT sweeps with every sweep's residual, a check
+                // finds the reference's early exit (model.rs:816), and the
+                // converged launch is re-run with exactly its sweeps
+                for (int it = 0; it < iters;) {
+                    int T, lo, hi, exch;
+                    plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
+                    launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream);
+                    launch_spec_check(g, f, pass, it, T, launches, stream);
+                    it += T;
+                    ++launches;
+                }
+                if (iters > 0) launch_jacobi_redo(g, f, pass, lo_g, hi_g, stream);
+            } else if (tmax <= 1) {
                 for (int it = 0; it < iters; ++it)
                     launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g,
                                         g.tol_enabled || it == iters - 1, stream);
@@ -863,7 +928,8 @@ struct cfd_model {
                                              pass >= 1 ? 1 : 0, launches};
             fin_pending = true;
         } else {
-            launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream);
+            launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream,
+                                  spec ? 2 : 0);
         }
         HIP_TRY(hipGetLastError());
         if (evt) {
@@ -957,6 +1023,19 @@ struct cfd_model {
     }
 
     bool host_driven() const { return sharded() && params.tol_enabled; }
+
+    // Speculative temporal blocking for the tolerance mode (single domain,
+    // Jacobi, p' allocation within kind 5's 1 GiB buffer range); CFD_SPEC=0
+    // keeps one launch per sweep with the per-sweep early exit.
+    bool spec_env = [] {
+        const char *e = getenv("CFD_SPEC");
+        return !(e && atoi(e) == 0);
+    }();
+    bool spec_mode() const {
+        return spec_env && !sharded() && g.tol_enabled &&
+               params.pressure_solver == CFD_SOLVER_JACOBI &&
+               (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)g.nx * 4u <= (1ull << 30);
+    }
 
     // piso_step (model.rs:529-730).
     // finish = inside update() with no extra corrector passes: the corrector,
@@ -1170,13 +1249,8 @@ struct cfd_model {
     void destroy() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        if (comm) {
-            // a non-blocking communicator finalises asynchronously: wait (under
-            // the deadline) for it, else abort instead of hanging in destroy
-            if (settle(ncclCommFinalize(comm), "ncclCommFinalize") == 0 && comm)
-                ncclCommDestroy(comm);
-            comm = nullptr;
-        }
+        if (comm) ncclCommDestroy(comm);
+        comm = nullptr;
         for (hipEvent_t e : ev_res)
             if (e) (void)hipEventDestroy(e);
         if (h_res) (void)hipHostFree(h_res);
@@ -1541,49 +1615,57 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     return 0;
 }
 
-// Communicator creation with a deadline: a non-blocking
-// ncclCommInitRankConfig, polled until every rank has joined or
-// CFD_RCCL_TIMEOUT_S passes (then aborted: CFD_ERCCL instead of hanging in
-// cfd_create_sharded when a peer never arrives).  CFD_RCCL_BLOCKING_INIT=1
-// restores the plain blocking ncclCommInitRank.
+// Communicator creation with a deadline.  ncclCommInitRank blocks in its
+// bootstrap until every rank has arrived, and RCCL's non-blocking config does
+// not change that (measured: ncclCommInitRankConfig with blocking = 0 did not
+// return while the peer was missing).  So the blocking call runs on a helper
+// thread and the caller waits at most CFD_RCCL_TIMEOUT_S: a rank that never
+// arrives makes cfd_create_sharded fail with CFD_ERCCL instead of hanging.
+// The stuck bootstrap is abandoned (the detached thread stays blocked; should
+// a late peer still complete it, the thread aborts that communicator itself).
+struct CommInitJob {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclSuccess;
+    hipError_t he = hipSuccess;
+};
+
 int comm_init(cfd_model *m, const ncclUniqueId &id, int n_ranks, int rank) {
-    const char *blk = getenv("CFD_RCCL_BLOCKING_INIT");
-    if (blk && atoi(blk) == 1) {
-        const ncclResult_t r = ncclCommInitRank(&m->comm, n_ranks, id, rank);
-        if (r != ncclSuccess) {
-            m->comm = nullptr;
-            return fail(CFD_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    auto job = std::make_shared<CommInitJob>();
+    const int device = m->device;
+    std::thread([job, id, n_ranks, rank, device] {
+        ncclComm_t c = nullptr;
+        ncclResult_t r = ncclInternalError;
+        const hipError_t he = hipSetDevice(device);
+        if (he == hipSuccess) r = ncclCommInitRank(&c, n_ranks, id, rank);
+        std::lock_guard<std::mutex> lk(job->mu);
+        if (job->abandoned) {
+            if (r == ncclSuccess && c) ncclCommAbort(c);
+            return;
         }
-        return 0;
+        job->comm = c;
+        job->r = r;
+        job->he = he;
+        job->done = true;
+        job->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(job->mu);
+    const auto limit = std::chrono::duration<double>(m->rccl_timeout_s);
+    if (!job->cv.wait_for(lk, limit, [&] { return job->done; })) {
+        job->abandoned = true;
+        return fail(CFD_ERCCL, "ncclCommInitRank: rank " + std::to_string(rank) + " of " +
+                                   std::to_string(n_ranks) + ": not every rank joined within " +
+                                   std::to_string((int)m->rccl_timeout_s) +
+                                   " s (CFD_RCCL_TIMEOUT_S); creation abandoned");
     }
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
-    ncclResult_t r = ncclCommInitRankConfig(&m->comm, n_ranks, id, rank, &cfg);
-    if (r != ncclSuccess && r != ncclInProgress) {
-        if (m->comm) ncclCommAbort(m->comm);
-        m->comm = nullptr;
-        return fail(CFD_ERCCL, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-        ncclResult_t st = ncclInProgress;
-        r = ncclCommGetAsyncError(m->comm, &st);
-        if (r == ncclSuccess) r = st;
-        if (r == ncclSuccess) return 0;
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (r != ncclInProgress || el > m->rccl_timeout_s) {
-            ncclCommAbort(m->comm);
-            m->comm = nullptr;
-            return fail(CFD_ERCCL,
-                        r != ncclInProgress
-                            ? std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r)
-                            : "ncclCommInitRankConfig: rank " + std::to_string(rank) + " of " +
-                                  std::to_string(n_ranks) + ": not every rank joined within " +
-                                  std::to_string((int)m->rccl_timeout_s) +
-                                  " s (CFD_RCCL_TIMEOUT_S); the communicator was aborted");
-        }
-        std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    }
+    if (job->he != hipSuccess)
+        return fail(CFD_EHIP, std::string("hipSetDevice (RCCL init thread): ") + hipGetErrorString(job->he));
+    if (job->r != ncclSuccess)
+        return fail(CFD_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(job->r));
+    m->comm = job->comm;
+    return 0;
 }
 
 int create_common(const cfd_grid *grid, const cfd_params *params, int device, int n_ranks, int rank,
@@ -2129,23 +2211,26 @@ int cfd_get_halo_depth(const cfd_model *m) { return m ? m->g.hg : 0; }
 int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal) {
     if (!m) return fail(CFD_EINVAL, "null model");
     if (fastdiv) *fastdiv = m->g.fastdiv;
-    if (temporal) *temporal = m->g.tol_enabled ? 1 : m->t_max;
+    if (temporal) *temporal = m->spec_mode() ? kMaxTemporal : m->g.tol_enabled ? 1 : m->t_max;
     return 0;
 }
 
 int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len) {
     if (!m) return fail(CFD_EINVAL, "null model");
-    const int T = m->g.tol_enabled ? 1 : m->t_max;
-    const int k = T <= 1 ? 0 : m->g.tb_kind;
+    const bool spec = m->spec_mode();
+    const int T = spec ? kMaxTemporal : m->g.tol_enabled ? 1 : m->t_max;
+    const int k = spec ? 5 : T <= 1 ? 0 : m->g.tb_kind;
     if (kind) *kind = k;
     if (name && name_len) {
         char buf[96];
-        if (k == 0)
+        if (spec)
+            snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, 2>", T, m->g.fastdiv);
+        else if (k == 0)
             snprintf(buf, sizeof buf, "k_jacobi<%d, %d>", kJacRowsPerWave, m->g.fastdiv);
         else if (k == 1)
             snprintf(buf, sizeof buf, "k_jacobi_tb<%d, %d>", T, m->g.fastdiv);
         else if (k == 5)
-            snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, false>", T, m->g.fastdiv);
+            snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, 0>", T, m->g.fastdiv);
         else
             snprintf(buf, sizeof buf, "k_jacobi_pipe<%d, %d, %d>", T, m->g.fastdiv, k == 3 ? 4 : 2);
         snprintf(name, name_len, "%s", buf);

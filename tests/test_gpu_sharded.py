@@ -309,12 +309,14 @@ def run_sharded_from_state(n, grid, params, state, steps):
 def test_sharded_full_size_developed_across_boundaries(n, nx, ny):
     """C4 (2 slabs of 8192x2048) and C5 (8 slabs of 16384x1024) at bench.py's
     default halo depth (32) from a DEVELOPED cavity: the single-domain model
-    runs 400 timed-mode steps, its state is injected into the slabs, and two
-    more steps on the slabs equal two more single-domain steps bit for bit.
-    Unlike 4 steps from rest, the rows either side of every slab boundary
-    now carry developed p' (>= 90 % non-zero), so the deep-halo exchange,
-    the overlapped bands and the rhs/u/v ghosts move real data.  For C4 one
-    step is also checked against the oracle from the developed state."""
+    runs 400 timed-mode steps, the state gets a seeded 1e-3 perturbation (so
+    boundaries deep below the lid, where p' has underflowed to 0, carry data
+    too), it is injected into the slabs, and two more steps on the slabs
+    equal two more single-domain steps bit for bit.  Unlike 4 steps from
+    rest, the rows either side of every slab boundary carry non-zero p'
+    (>= 90 %), so the deep-halo exchange, the overlapped bands and the
+    rhs/u/v ghosts move real data.  For C4 one step is also checked against
+    the oracle from the same state."""
     import cfdamd
     grid = cfdamd.cavity_grid(nx, ny)
     params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
@@ -322,10 +324,18 @@ def test_sharded_full_size_developed_across_boundaries(n, nx, ny):
     try:
         m.update_n(400)
         st0 = m.get_state()
+        # the cavity develops from the lid down (p' underflows to 0 far below
+        # it): a seeded 1e-3 perturbation puts data in every boundary row
+        rng = np.random.default_rng(1234)
+        for k in ("u", "v", "u_star", "v_star", "p_prime"):
+            st0[k] = (st0[k] + (1e-3 * rng.uniform(-1.0, 1.0, st0[k].size)).astype(
+                np.float32)).astype(np.float32)
+        m.set_state(**st0)
         m.update_n(2)
         ref = m.get_state()
     finally:
         m.close()
+    assert np.isfinite(ref["u"]).all() and np.isfinite(ref["p_prime"]).all()
     pp = st0["p_prime"].reshape(ny, nx)
     import ctypes as C
     L = cfdamd.load()

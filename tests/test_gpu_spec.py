@@ -1,0 +1,124 @@
+"""GPU: speculative temporal blocking of the reference's tolerance mode.
+
+With the tolerance on (model.rs:748-819: <= 50 sweeps, early exit once
+max |dp'| < p_tol, up to 20 re-correction passes) a single-domain Jacobi
+solve runs T = 8 sweeps per kind-5 launch and publishes every sweep's
+residual; k_spec_check finds the first sweep below p_tol, stops the later
+launches and, when that sweep is not the launch's last, re-runs the launch
+from its untouched source buffer with exactly that many sweeps.  The result
+must be the reference's bit for bit: every field, every scalar, and the sweep
+count (jacobi_sweeps_total), step by step against the oracle, on grids and
+tolerances that make solves stop at every possible stage of a launch.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from _util import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+STATE = ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
+
+
+@pytest.fixture(autouse=True)
+def _oracle_threads():
+    import oracle
+    try:
+        n = max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        n = 4
+    oracle.set_threads(n)
+    yield
+    oracle.set_threads(1)
+
+
+def _compare(tag, m, o):
+    st = m.get_state()
+    for f in STATE:
+        assert_bitwise(f"{tag}:{f}", st[f], o.field(f))
+    s = o.scalars()
+    assert st["simulation_step"] == s.step, tag
+    assert st["jacobi_sweeps_total"] == s.jacobi_sweeps_total, (tag, st["jacobi_sweeps_total"],
+                                                               s.jacobi_sweeps_total)
+    for k, want in (("simulation_time", s.time), ("dt", s.dt), ("last_p_residual", s.p),
+                    ("last_u_residual", s.u), ("last_v_residual", s.v)):
+        assert np.float32(st[k]).view(np.uint32) == np.float32(want).view(np.uint32), (tag, k)
+    return int(s.jacobi_sweeps_total)
+
+
+def _run(grid, params, okw, steps, tag):
+    import cfdamd
+    from oracle import OracleModel
+    c = grid.obstacle
+    m = cfdamd.Model(grid, params, device=0)
+    assert m.kernel_config["temporal"] == 8, m.kernel_config
+    assert m.jacobi_kernel["name"].startswith("k_jacobi_lds<8,"), m.jacobi_kernel
+    o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly,
+                    cylinder=(c.center_x, c.center_y, c.radius) if c else None, **okw)
+    sweeps = []
+    try:
+        prev = 0
+        for k in range(steps):
+            m.update()
+            o.update()
+            tot = _compare(f"{tag} step {k + 1}", m, o)
+            sweeps.append(tot - prev)
+            prev = tot
+    finally:
+        m.close()
+    return sweeps
+
+
+@pytest.mark.parametrize("p_tol", [1e-4, 1e-3, 3e-5])
+def test_spec_cavity_parity_mode(p_tol):
+    """128^2 cavity, Re 100, the reference's control flow at three tolerances:
+    solves end early at varying sweeps (the re-run with 1..7 sweeps)."""
+    import cfdamd
+    params = cfdamd.SimulationParams.cavity(100.0, 50, p_tol=p_tol)
+    sweeps = _run(cfdamd.cavity_grid(128), params,
+                  dict(bc_kind=1, viscosity=0.01, p_tol=p_tol), 40, f"cavity tol {p_tol}")
+    # the early exit was taken: not every step ran whole 8-sweep launches
+    assert any(s % 8 for s in sweeps), sweeps
+
+
+def test_spec_channel_default_grid_cylinder():
+    """The reference's default grid (800 x 264 channel, cylinder, src/app.rs
+    :33-53) with its default parameters (SimulationParams::default)."""
+    import cfdamd
+    _run(cfdamd.default_grid(), cfdamd.SimulationParams(), {}, 12, "default channel")
+
+
+def test_spec_channel_second_order_parabolic():
+    import cfdamd
+    grid = cfdamd.Grid(256, 96, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5))
+    params = cfdamd.SimulationParams(velocity_scheme=cfdamd.VelocityScheme.SecondOrder,
+                                     inlet_profile=cfdamd.InletProfile.Parabolic)
+    _run(grid, params, dict(scheme=1, inlet_profile=1), 20, "channel SO")
+
+
+def test_spec_c2_parity_mode():
+    """C2 (1024^2 cavity, Re 400) in the reference's control flow."""
+    import cfdamd
+    params = cfdamd.SimulationParams.cavity(400.0, 50)
+    _run(cfdamd.cavity_grid(1024), params, dict(bc_kind=1, viscosity=0.0025), 6, "C2 parity")
+
+
+def test_spec_off_matches_spec_on(monkeypatch):
+    """CFD_SPEC=0 (one launch per sweep with the per-sweep early exit) and the
+    speculative path give the same bits and sweep counts."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(256, 128)
+    params = cfdamd.SimulationParams.cavity(400.0, 50, p_tol=2e-4)
+    states = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("CFD_SPEC", env)
+        m = cfdamd.Model(grid, params, device=0)
+        assert m.kernel_config["temporal"] == (1 if env == "0" else 8)
+        m.update_n(15)
+        states.append(m.get_state())
+        m.close()
+    for f in STATE:
+        assert_bitwise(f"spec on/off:{f}", states[1][f], states[0][f])
+    assert states[0]["jacobi_sweeps_total"] == states[1]["jacobi_sweeps_total"]

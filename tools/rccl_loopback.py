@@ -126,10 +126,23 @@ def slab_slices(st, nx, j0, j1):
     return out
 
 
+def perturb(st, np, seed=1234, amp=1e-3):
+    """Add a seeded f32 perturbation of amplitude `amp` to the developed u, v,
+    u*, v* and p' (the same bits on every rank).  The cavity develops from the
+    lid down and p' underflows to exactly 0 far below it, so slab boundaries
+    deep in the grid would otherwise carry zeros; this puts non-zero data in
+    every row a halo exchange moves."""
+    rng = np.random.default_rng(seed)
+    for k in ("u", "v", "u_star", "v_star", "p_prime"):
+        st[k] = (st[k] + (amp * rng.uniform(-1.0, 1.0, st[k].size)).astype(np.float32)).astype(
+            np.float32)
+
+
 def developed(args, rank, n, cfdamd, dist, np):
     """The bench's timed mode on a DEVELOPED cavity: every rank develops the
     single-domain model for --develop steps (deterministic, so every rank
-    holds the same bits), injects its slab rows into the RCCL-sharded model
+    holds the same bits), perturbs it (perturb), injects its slab rows into the
+    RCCL-sharded model
     (cfd_set_state exchanges the ghosts), and runs --steps steps; its rows
     must equal the single-domain continuation bit for bit.  The slab
     boundaries carry developed p' (the non-zero fraction of the rows either
@@ -140,6 +153,9 @@ def developed(args, rank, n, cfdamd, dist, np):
     ref = cfdamd.Model(grid, params, device=0)
     ref.update_n(args.develop)
     st0 = ref.get_state()
+    nz_dev = float(np.count_nonzero(st0["p_prime"])) / st0["p_prime"].size
+    perturb(st0, np)
+    ref.set_state(**st0)
     ref.update_n(args.steps)
     want = ref.get_state()
     ref.close()
@@ -167,6 +183,7 @@ def developed(args, rank, n, cfdamd, dist, np):
                       "grid": [args.nx, args.ny], "slab": [j0, j1], "develop": args.develop,
                       "steps": args.steps, "boundary_rows": rows,
                       "boundary_pprime_nonzero_frac": nzf,
+                      "developed_pprime_nonzero_frac": nz_dev,
                       "bitwise_equal_single_domain": not bad, "differ": bad,
                       "sharded_wall_s": round(el, 3)}), flush=True)
     dist.barrier()
