@@ -128,6 +128,9 @@ struct Fields {
 // pass < 0 means "not inside the corrector loop" (always runs).
 void launch_step_begin(const Geom &g, const Fields &f, int copy, hipStream_t s);
 void launch_copy_star(const Geom &g, const Fields &f, int pass, hipStream_t s);
+// k_copy_star + k_divergence of a corrector pass in one launch (same values).
+void launch_copy_star_div(const Geom &g, const Fields &f, int pass, float dt_override,
+                          hipStream_t s);
 void launch_u_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_v_predictor(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 // u and v predictors in one pass (same results as the two launches above).
@@ -222,11 +225,15 @@ struct SorConst {
 // current / other p' buffer), right-hand side, residual scratch, size and the
 // level's constants (spacing 2^l times the model's, index.html:1458).
 struct MgLevel {
+    // biased to global row 0: element (i, j) of the level is a[j * nx + i]
+    // for every stored row j in [ys, ye)
     float *a, *b, *rhs, *r;
-    int32_t nx, ny;
+    int32_t nx, ny;        // the level's global size
     double dx2, dy2, denom;
     double r_dx2, r_dy2, r_denom;
     int32_t fast;
+    int32_t ys, ye;        // stored rows (a slab's rows + ghost rows; 0, ny unsharded)
+    int32_t lo, hi;        // rows a launch outputs (set per launch; 0, ny unsharded)
 };
 constexpr int kMgMaxLevels = 40;
 void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorConst &k, int color,

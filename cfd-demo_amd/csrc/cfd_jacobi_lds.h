@@ -72,16 +72,23 @@ __device__ unsigned long long g_lds_stamp[kStampWaves * 4];
 #define CFD_LDS_HOIST 0  // 1: read a slot's T rhs rows from the LDS ring at its start (r2: 5.09 vs 5.00 us/sweep, off)
 #endif
 
-#ifndef CFD_LDS_LAG
-#define CFD_LDS_LAG 1  // rows between consecutive stages of one slot (see LdsMarch)
+#ifndef CFD_LDS_SPLIT
+#define CFD_LDS_SPLIT 1  // independent stage groups per slot (see LdsMarch)
 #endif
 constexpr int lds_gcd(int a, int b) { return b == 0 ? a : lds_gcd(b, a % b); }
-// rhs ring depth: the smallest multiple of lcm(NW, PD) that holds L*T+1 rows
-// (NW = L+2 rows of each stage's register window)
-constexpr int ring_depth(int T, int PD, int L) {
-    const int nw = L + 2;
+// Slots of lag accumulated before stage s when the T stages form G groups,
+// each group one slot behind the one before it.
+constexpr int lds_off(int s, int T, int G) { return s <= 0 ? 0 : ((s - 1) * G) / T; }
+// register window rows per stage: 3, or 4 when a stage reads its
+// predecessor's rows one slot late
+constexpr int lds_nw(int G) { return G > 1 ? 4 : 3; }
+// rhs ring depth: the smallest multiple of lcm(NW, PD) holding the T + off(T)
+// + 1 rows between the newest load and the last stage's read
+constexpr int ring_depth(int T, int PD, int G) {
+    const int nw = lds_nw(G);
     const int q = nw / lds_gcd(nw, PD) * PD;
-    return ((L * T + 1 + q - 1) / q) * q;
+    const int need = T + lds_off(T, T, G) + 1;
+    return ((need + q - 1) / q) * q;
 }
 
 // MODE: 0 plain launch; 1 (RES) the solve's last launch, publishes the last
@@ -93,23 +100,28 @@ constexpr int ring_depth(int T, int PD, int L) {
 template <int T, int FAST, int MODE>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1, SPEC = MODE == 2, REDO = MODE == 3;
-    // Lag L: stage s of slot v computes row k - L*s.  L = 1 is the plain
-    // pipeline (stage s reads stage s-1's row of the SAME slot: one serial
-    // chain of T updates per slot).  L = 2 skews the stages so that stage s
-    // reads only rows stage s-1 finished in EARLIER slots: the T updates of a
-    // slot are independent and the wave has T-way instruction-level
-    // parallelism, for one more row per stage in registers (NW = L+2) and an
-    // rhs window of L*T+1 rows.  The set of (stage, row) updates is the same.
-    static constexpr int L = CFD_LDS_LAG;
-    static constexpr int NW = L + 2;               // register window rows per stage
-    static constexpr int PD = CFD_LDS_PD;          // prefetch distance (slots) of p' and rhs
-    static constexpr int D = ring_depth(T, PD, L); // rhs ring depth; PD and NW divide it
-    static constexpr int U = D;                    // slot unroll: every ring index compile-time
-    static constexpr int WARM = (L + 1) * T;       // stage s starts at slot (L+1)*s
-    static constexpr int H = (T + 1) / 2;          // halo lanes per side (2 columns per lane)
-    static constexpr int OUTL = 64 - 2 * H;        // lanes whose columns are stored
-    static_assert(D % PD == 0 && D % NW == 0 && D >= L * T + 1, "ring geometry");
-    static_assert(L == 1 || L == 2, "lag");
+    // Stage s of slot v computes row k - s - off(s).  With G = 1 (off = 0)
+    // this is the plain pipeline: stage s reads stage s-1's row of the SAME
+    // slot, one serial chain of T dependent updates per slot.  With G > 1 the
+    // stages form G groups and each group runs one slot behind the previous
+    // one: a group's first stage reads rows its predecessor finished in an
+    // EARLIER slot, so a slot holds G independent chains of T/G updates (ILP
+    // that hides the packed-f32 result latency), for one more window row per
+    // stage (NW = 4) and off(T) more warm-up and ring rows.  The set of
+    // (stage, row) updates is the same, and so is every value.
+    static constexpr int G = CFD_LDS_SPLIT;
+    static constexpr int NW = lds_nw(G);            // register window rows per stage
+    static constexpr int PD = CFD_LDS_PD;           // prefetch distance (slots) of p' and rhs
+    static constexpr int OFFT = lds_off(T, T, G);
+    static constexpr int D = ring_depth(T, PD, G);  // rhs ring depth; PD and NW divide it
+    static constexpr int U = D;                     // slot unroll: every ring index compile-time
+    static constexpr int WARM = 2 * T + OFFT;       // stage s starts at slot 2s + off(s)
+    static constexpr int H = (T + 1) / 2;           // halo lanes per side (2 columns per lane)
+    static constexpr int OUTL = 64 - 2 * H;         // lanes whose columns are stored
+    static constexpr int off(int s) { return lds_off(s, T, G); }
+    static constexpr int start(int s) { return 2 * s + off(s); }
+    static_assert(D % PD == 0 && D % NW == 0 && D >= T + OFFT + 1, "ring geometry");
+    static_assert(G >= 1 && G <= T, "stage groups");
 
     f2 W[T][NW];
     f2 PQ[PD];
@@ -181,7 +193,7 @@ struct LdsMarch {
     }
 
     // Slot v (k = k_first + v), V_ == v (mod U).  GUARD 0: warm-up (V_ == v,
-    // stage s runs from slot (L+1)s on); GUARD 2: the final partial group;
+    // stage s runs from slot start(s) on); GUARD 2: the final partial group;
     // GUARD 3: both, decided at run time (CFD_LDS_COMPACT).
     template <int V_, int GUARD, int E>
     __device__ __forceinline__ void slot(int v) {
@@ -199,22 +211,24 @@ struct LdsMarch {
         f2 rhv[T];
         if (CFD_LDS_HOIST && !(CFD_LDS_DIAG & 2)) {
 #pragma unroll
-            for (int s = 1; s <= T; ++s) rhv[s - 1] = ring[((V_ - L * s + 8 * D) % D) * 64 + lane];
+            for (int s = 1; s <= T; ++s) rhv[s - 1] = ring[((V_ - s - off(s) + 8 * D) % D) * 64 + lane];
         }
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
-            if (GUARD == 0 && V_ < (L + 1) * s) continue;            // compile-time
-            if (GUARD == 3 && v < (L + 1) * s) continue;             // wave-uniform
+            if (GUARD == 0 && V_ < start(s)) continue;               // compile-time
+            if (GUARD == 3 && v < start(s)) continue;                // wave-uniform
             if (CFD_LDS_SB >= 2 && s > 1) __builtin_amdgcn_sched_barrier(0);
-            const int r = k - L * s;
+            const int r = k - s - off(s);
             const f2 rh = (CFD_LDS_DIAG & 2) ? RQ[(V_ + s) % PD]
                                              : (CFD_LDS_HOIST ? rhv[s - 1]
-                                                              : ring[((V_ - L * s + 8 * D) % D) * 64 + lane]);
-            // stage s-1 finished row x at slot x - k_first + L(s-1)
+                                                              : ring[((V_ - s - off(s) + 8 * D) % D) * 64 + lane]);
+            // stage s-1 finished row r+1 in slot v - dl (dl = 0 inside a
+            // group, 1 at a group's first stage), row r one slot earlier, ...
             constexpr int kW = 4 * NW;
-            const f2 &B = W[s - 1][(V_ - L - 1 + kW) % NW];          // stage s-1, row r-1
-            const f2 &C = W[s - 1][(V_ - L + kW) % NW];              //            row r
-            const f2 &Tp = W[s - 1][(V_ + 1 - L + kW) % NW];         //            row r+1
+            const int dl = off(s) - off(s - 1);
+            const f2 &B = W[s - 1][(V_ - dl - 2 + kW) % NW];         // stage s-1, row r-1
+            const f2 &C = W[s - 1][(V_ - dl - 1 + kW) % NW];         //            row r
+            const f2 &Tp = W[s - 1][(V_ - dl + kW) % NW];            //            row r+1
             if (REDO && s > nst) continue;                            // wave-uniform
             f2 n = stage<E>(B, C, Tp, rh);
             if (SPEC && r >= r0v && r < r1v) {
@@ -444,7 +458,7 @@ __global__ CFD_LDS_BOUNDS void k_jacobi_lds(
     // all boundary logic
     const int ch_lo = wc * M::OUTL - M::H, ch_hi = ch_lo + 63;
     const bool col_edge = ch_lo <= 0 || 2 * (ch_hi + 1) > nx - 8;
-    const int lo_row = w.k_first - 2, hi_row = r1 + M::L * T + 2;   // every row a stage computes
+    const int lo_row = w.k_first - 2, hi_row = r1 + T + M::OFFT + 2;   // every row a stage computes
     auto hits = [&](int r) { return r >= lo_row && r <= hi_row; };
     const bool row_edge = hits(w.g_zero) || hits(w.g_first) || hits(w.g_last) || hits(w.g_top);
     const bool edge = col_edge || row_edge;

@@ -325,6 +325,45 @@ __global__ __launch_bounds__(kBlock) void k_divergence(Geom g, Fields f, int pas
     *reinterpret_cast<float4 *>(f.rhs + (long)lj * nx + i0) = r;
 }
 
+// The head of a corrector-loop pass (model.rs:698-704): u* <- u, v* <- v and
+// rhs = div(u*, v*) / dt in one pass.  The divergence is formed from the u
+// and v values the copy has just read (they are the new u*, v*), so u* and v*
+// are not read back: 20 B per cell instead of the 28 of k_copy_star +
+// k_divergence, and one launch.  A thread owns 4 cells of one allocation row;
+// ghost rows are copied too (k_copy_star copies whole allocations), owned rows
+// also get rhs, with k_divergence's arithmetic bit for bit.
+template <int SP>
+__global__ __launch_bounds__(kBlock) void k_copy_star_div(Geom g, Fields f, int pass,
+                                                          float dt_override, int nbx) {
+    if (pass_off(f.ctl, pass)) return;
+    const int bid = xcd_block(g);
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
+    const int lr = bid / nbx - kGhostUV;   // local row: v rows -G..nyl+G, u rows -G..nyl+G-1
+    const int nx = g.nx, W = nx + 1;
+    if (i0 >= nx) return;
+    const float4 vs = *reinterpret_cast<const float4 *>(f.v + (long)lr * nx + i0);
+    *reinterpret_cast<float4 *>(f.v_star + (long)lr * nx + i0) = vs;
+    if (lr >= g.nyl + kGhostUV) return;   // v's extra face row
+    const float *__restrict__ ur = f.u + (long)lr * W + i0;
+    float *__restrict__ us = f.u_star + (long)lr * W + i0;
+    const float u0 = ur[0], u1 = ur[1], u2 = ur[2], u3 = ur[3], u4 = ur[4];
+    us[0] = u0;
+    us[1] = u1;
+    us[2] = u2;
+    us[3] = u3;
+    if (i0 + 4 == nx) us[4] = u4;   // face nx
+    if (lr < 0 || lr >= g.nyl) return;
+    const float4 vn = *reinterpret_cast<const float4 *>(f.v + (long)(lr + 1) * nx + i0);
+    const float dt = dt_of(f.ctl, dt_override);
+    const float rdx = g.r_dx, rdy = g.r_dy, dx = g.dx, dy = g.dy;
+    float4 r;
+    r.x = (sdiv<SP>(u1 - u0, dx, rdx) + sdiv<SP>(vn.x - vs.x, dy, rdy)) / dt;
+    r.y = (sdiv<SP>(u2 - u1, dx, rdx) + sdiv<SP>(vn.y - vs.y, dy, rdy)) / dt;
+    r.z = (sdiv<SP>(u3 - u2, dx, rdx) + sdiv<SP>(vn.z - vs.z, dy, rdy)) / dt;
+    r.w = (sdiv<SP>(u4 - u3, dx, rdx) + sdiv<SP>(vn.w - vs.w, dy, rdy)) / dt;
+    *reinterpret_cast<float4 *>(f.rhs + (long)lr * nx + i0) = r;
+}
+
 // ------------------------------------------- predict + divergence (K1-K3)
 
 // Both first-order predictors and the divergence in one pass (piso_step
@@ -1371,6 +1410,16 @@ void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipSt
         if (g.sp_pow2) CFD_LAUNCH_PD(1, 2); else CFD_LAUNCH_PD(0, 2);
     }
 #undef CFD_LAUNCH_PD
+}
+
+void launch_copy_star_div(const Geom &g, const Fields &f, int pass, float dt_override,
+                          hipStream_t s) {
+    const int nbx = cdiv(g.nx / 4, kBlock);
+    const dim3 grid(nbx * (g.nyl + 1 + 2 * kGhostUV));
+    if (g.sp_pow2)
+        hipLaunchKernelGGL(k_copy_star_div<1>, grid, dim3(kBlock), 0, s, g, f, pass, dt_override, nbx);
+    else
+        hipLaunchKernelGGL(k_copy_star_div<0>, grid, dim3(kBlock), 0, s, g, f, pass, dt_override, nbx);
 }
 
 void launch_divergence(const Geom &g, const Fields &f, int pass, float dt_override,

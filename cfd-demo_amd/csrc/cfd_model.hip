@@ -13,6 +13,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <initializer_list>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -596,6 +597,49 @@ struct cfd_model {
     // Level table of mgVcycle's recursion: sizes floor((n+1)/2) down to the
     // first level with nx <= 4 or ny <= 4 (index.html:1444-1451), spacing
     // doubling per level (:1458).
+    //
+    // Sharded models partition the fine levels too (mg_P levels; see
+    // enqueue_mg_partitioned): level l of rank r owns global rows
+    // [J0 / 2^l, J1 / 2^l) of its slab [J0, J1) and stores kMgGhost ghost
+    // rows each side.  A level is partitioned when every rank's boundary is
+    // divisible by 2^(l+1) (the restriction maps owned rows onto owned rows),
+    // every slab keeps >= 2 kMgGhost rows there, and the level lies above the
+    // single-workgroup tail; the coarser levels are gathered whole to every
+    // rank.  Every level pointer is biased to global row 0.
+    static constexpr int kMgGhost = 8;   // >= 7: 5 sweeps + residual + the restriction's row
+    int mg_P = 0;
+    bool mg_part_env = [] {
+        const char *e = getenv("CFD_MG_PARTITION");
+        return !(e && atoi(e) == 0);
+    }();
+    // owned rows of level l for `rank` (partitioned levels)
+    void mg_rows(int l, int r, int *j0o, int *j1o) const {
+        uint64_t a, b;
+        plan_slab(g.ny, n_ranks, r, &a, &b);
+        *j0o = (int)(a >> l);
+        *j1o = r == n_ranks - 1 ? mg[l].ny : (int)(b >> l);
+    }
+    int mg_partition_levels(const std::vector<std::pair<int, int>> &dims, int tail) const {
+        if (!sharded() || !mg_part_env || !mg_smooth_wave_form()) return 0;
+        if (const char *e = getenv("CFD_MG_TB"))
+            if (atoi(e) == 0) return 0;
+        int P = 0;
+        for (int l = 0; l < tail && l + 1 < (int)dims.size(); ++l) {
+            bool ok = true;
+            for (int r = 0; r < n_ranks && ok; ++r) {
+                uint64_t a, b;
+                plan_slab(g.ny, n_ranks, r, &a, &b);
+                const uint64_t m = 1ull << (l + 1);
+                const int j0l = (int)(a >> l);
+                const int j1l = r == n_ranks - 1 ? dims[l].second : (int)(b >> l);
+                ok = a % m == 0 && j1l - j0l >= 2 * kMgGhost;
+            }
+            if (!ok) break;
+            P = l + 1;
+        }
+        return P;
+    }
+
     int mg_build() {
         if (!mg.empty()) return 0;
         std::vector<std::pair<int, int>> dims{{g.nx, g.ny}};
@@ -604,39 +648,56 @@ struct cfd_model {
             dims.push_back({(dims.back().first + 1) / 2, (dims.back().second + 1) / 2});
         }
         const int nl = (int)dims.size();
-        // level 0: the residual; a sharded model also keeps full-grid
-        // solution buffers and the gathered rhs (every rank solves the whole
-        // grid redundantly, see enqueue_mg)
-        size_t total = (sharded() ? 4 : 1) * round4((size_t)g.nx * g.ny);
-        for (int l = 1; l < nl; ++l) total += 4 * round4((size_t)dims[l].first * dims[l].second);
+        // levels of at most CFD_MG_TAIL cells (default 64 x 64) run inside k_mg_tail
+        long thr = 4096;
+        if (const char *e = getenv("CFD_MG_TAIL")) thr = atol(e);
+        mg_tail = nl - 1;
+        for (int l = 0; l < nl; ++l)
+            if ((long)dims[l].first * dims[l].second <= thr) {
+                mg_tail = l;
+                break;
+            }
+        mg_P = mg_partition_levels(dims, mg_tail);
+        mg.resize(nl);
+        for (int l = 0; l < nl; ++l) {
+            std::memset(&mg[l], 0, sizeof(MgLevel));
+            mg[l].nx = dims[l].first;
+            mg[l].ny = dims[l].second;
+            mg[l].ys = 0;
+            mg[l].ye = mg[l].ny;
+            if (l < mg_P) {
+                int a, b;
+                mg_rows(l, rank, &a, &b);
+                mg[l].ys = std::max(0, a - kMgGhost);
+                mg[l].ye = std::min(mg[l].ny, b + kMgGhost);
+            }
+        }
+        // level 0: the residual; a sharded model also keeps its own solution
+        // buffers and rhs (the gathered whole grid when no level partitions:
+        // every rank then solves the whole grid redundantly, see enqueue_mg)
+        auto rows_of = [&](int l) { return (size_t)(mg[l].ye - mg[l].ys); };
+        size_t total = (sharded() ? 4 : 1) * round4((size_t)g.nx * rows_of(0));
+        for (int l = 1; l < nl; ++l) total += 4 * round4((size_t)dims[l].first * rows_of(l));
         HIP_TRY(hipMalloc((void **)&mg_pool, total * 4));
         HIP_TRY(hipMemsetAsync(mg_pool, 0, total * 4, stream));
         float *cur = mg_pool;
-        auto take = [&](size_t n) {
-            float *p0 = cur;
-            cur += round4(n);
-            return p0;
-        };
-        mg.resize(nl);
         for (int l = 0; l < nl; ++l) {
             MgLevel &L = mg[l];
-            std::memset(&L, 0, sizeof(L));
-            L.nx = dims[l].first;
-            L.ny = dims[l].second;
-            const size_t n = (size_t)L.nx * L.ny;
-            if (l == 0 && sharded()) {
-                L.a = take(n);
-                L.b = take(n);
-                L.rhs = take(n);
-                L.r = take(n);
-            } else if (l == 0) {
+            const size_t n = (size_t)L.nx * rows_of(l);
+            const long bias = (long)L.ys * L.nx;   // pointers address global rows
+            auto take = [&]() {
+                float *p0 = cur - bias;
+                cur += round4(n);
+                return p0;
+            };
+            if (l == 0 && !sharded()) {
                 L.rhs = f.rhs;
-                L.r = take(n);
+                L.r = take();
             } else {
-                L.a = take(n);
-                L.b = take(n);
-                L.rhs = take(n);
-                L.r = take(n);
+                L.a = take();
+                L.b = take();
+                L.rhs = take();
+                L.r = take();
             }
             const double scale = std::ldexp(1.0, l);   // 2*dx per recursion, exact
             double r[3];
@@ -645,16 +706,9 @@ struct cfd_model {
             L.r_dx2 = r[0];
             L.r_dy2 = r[1];
             L.r_denom = r[2];
+            L.lo = L.ys;
+            L.hi = L.ye;
         }
-        // levels of at most CFD_MG_TAIL cells (default 64 x 64) run inside k_mg_tail
-        long thr = 4096;
-        if (const char *e = getenv("CFD_MG_TAIL")) thr = atol(e);
-        mg_tail = nl - 1;
-        for (int l = 0; l < nl; ++l)
-            if ((long)mg[l].nx * mg[l].ny <= thr) {
-                mg_tail = l;
-                break;
-            }
         HIP_TRY(hipMalloc((void **)&mg_dev, sizeof(MgLevel) * nl));
         HIP_TRY(hipMemcpy(mg_dev, mg.data(), sizeof(MgLevel) * nl, hipMemcpyHostToDevice));
         return 0;
@@ -695,11 +749,205 @@ struct cfd_model {
         return 0;
     }
 
+    // ---- multigrid on slabs with partitioned fine levels (mg_P > 0) ----
+    // Ghost rows of level arrays with both neighbours (which: 0 a, 1 b, 2 rhs):
+    // rows [J0-d, J0) come from rank-1's owned rows, [J1, J1+d) from rank+1's,
+    // every item in one RCCL group (LocalHub: device copies from the peers).
+    struct MgX {
+        int l, which, depth;
+    };
+    static float *mg_arr(const MgLevel &L, int which) {
+        return which == 0 ? L.a : which == 1 ? L.b : L.rhs;
+    }
+    int mg_exchange(std::initializer_list<MgX> items) {
+        if (hub) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();   // every member's rows are final
+            for (const MgX &x : items) {
+                const size_t nx = (size_t)mg[x.l].nx, d = (size_t)x.depth;
+                int j0, j1;
+                mg_rows(x.l, rank, &j0, &j1);
+                float *mine = mg_arr(mg[x.l], x.which);
+                if (rank > 0) {
+                    const float *peer = mg_arr(hub->members[rank - 1]->mg[x.l], x.which);
+                    HIP_TRY(hipMemcpyAsync(mine + (j0 - (long)d) * nx, peer + (j0 - (long)d) * nx,
+                                           d * nx * 4, hipMemcpyDeviceToDevice, stream));
+                }
+                if (rank < n_ranks - 1) {
+                    const float *peer = mg_arr(hub->members[rank + 1]->mg[x.l], x.which);
+                    HIP_TRY(hipMemcpyAsync(mine + (long)j1 * nx, peer + (long)j1 * nx, d * nx * 4,
+                                           hipMemcpyDeviceToDevice, stream));
+                }
+            }
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();   // nobody overwrites rows a peer is still copying
+            return 0;
+        }
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        RCCL_TRY(ncclGroupStart());
+        for (const MgX &x : items) {
+            const size_t nx = (size_t)mg[x.l].nx, n = (size_t)x.depth * nx;
+            int j0, j1;
+            mg_rows(x.l, rank, &j0, &j1);
+            float *a = mg_arr(mg[x.l], x.which);
+            if (rank > 0) {
+                RCCL_OP(ncclSend(a + (long)j0 * nx, n, ncclFloat, rank - 1, comm, stream));
+                RCCL_OP(ncclRecv(a + (long)(j0 - x.depth) * nx, n, ncclFloat, rank - 1, comm, stream));
+            }
+            if (rank < n_ranks - 1) {
+                RCCL_OP(ncclSend(a + (long)(j1 - x.depth) * nx, n, ncclFloat, rank + 1, comm, stream));
+                RCCL_OP(ncclRecv(a + (long)j1 * nx, n, ncclFloat, rank + 1, comm, stream));
+            }
+        }
+        RCCL_OP(ncclGroupEnd());
+        return 0;
+    }
+    // every rank's owned rows of the (whole, not partitioned) level l's rhs
+    int mg_allgather_rhs(int l) {
+        const size_t nx = (size_t)mg[l].nx;
+        int j0, j1;
+        mg_rows(l, rank, &j0, &j1);
+        if (hub) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();
+            for (int r = 0; r < n_ranks; ++r) {
+                if (r == rank) continue;
+                int a, b;
+                mg_rows(l, r, &a, &b);
+                HIP_TRY(hipMemcpyAsync(mg[l].rhs + (long)a * nx, hub->members[r]->mg[l].rhs + (long)a * nx,
+                                       (size_t)(b - a) * nx * 4, hipMemcpyDeviceToDevice, stream));
+            }
+            HIP_TRY(hipStreamSynchronize(stream));
+            hub->barrier();
+            return 0;
+        }
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        RCCL_TRY(ncclGroupStart());
+        for (int r = 0; r < n_ranks; ++r) {
+            if (r == rank) continue;
+            int a, b;
+            mg_rows(l, r, &a, &b);
+            RCCL_OP(ncclSend(mg[l].rhs + (long)j0 * nx, (size_t)(j1 - j0) * nx, ncclFloat, r, comm, stream));
+            RCCL_OP(ncclRecv(mg[l].rhs + (long)a * nx, (size_t)(b - a) * nx, ncclFloat, r, comm, stream));
+        }
+        RCCL_OP(ncclGroupEnd());
+        return 0;
+    }
+
+    // The V-cycles (index.html:1444-1470) with levels 0..P-1 partitioned:
+    // down  each rank smooths (5 sweeps) and forms the residual over its rows
+    //       plus the row below (the restriction reads it), restricts onto its
+    //       coarse rows and exchanges that level's rhs ghosts; level P is
+    //       gathered whole (all-gather of the restricted rhs rows);
+    // coarse levels P..Lc run whole on every rank with the single-domain
+    //       kernels and the tail (identical arithmetic on identical data);
+    // up    each rank exchanges its pre-smoothed field's 5 ghost rows (and
+    //       the coarse correction's 3), prolong-adds and smooths its rows.
+    // Every level-l row is computed from the same values as in the
+    // single-domain solve, so the result is bitwise the same; the whole grid
+    // is touched only on the small gathered levels.
+    int enqueue_mg_partitioned(int pass, float *residual_out, hipEvent_t e0) {
+        const int lc = (int)mg.size() - 1, P = mg_P;
+        int J0[kMgMaxLevels + 1], J1[kMgMaxLevels + 1];
+        for (int l = 0; l <= P; ++l) mg_rows(l, rank, &J0[l], &J1[l]);
+        auto lvl = [&](int l, int lo, int hi) {
+            MgLevel L = mg[l];
+            L.lo = lo;
+            L.hi = hi;
+            return L;
+        };
+        // (the allocation of a level array is rounded up to 4 floats)
+        auto zero = [&](const MgLevel &L) {
+            launch_fill_zero(L.a + (long)L.ys * L.nx, round4((size_t)(L.ye - L.ys) * L.nx), f.ctl, pass,
+                             stream);
+        };
+        const size_t nx = (size_t)g.nx;
+        int launches = 1;
+        // level 0: the slab's rhs rows and their ghosts; p' = 0 (index.html:777)
+        HIP_TRY(hipMemcpyAsync(mg[0].rhs + (long)J0[0] * nx, f.rhs, (size_t)g.nyl * nx * 4,
+                               hipMemcpyDeviceToDevice, stream));
+        zero(mg[0]);
+        int rc = mg_exchange({{0, 2, kMgGhost}});
+        if (rc) return rc;
+        for (int cycle = 0; cycle < 3; ++cycle) {
+            if (cycle > 0) {   // the last up-leg wrote level 0's rows only
+                rc = mg_exchange({{0, 0, kMgGhost}});
+                if (rc) return rc;
+            }
+            for (int l = 0; l < P; ++l) {
+                const MgLevel L = lvl(l, std::max(0, J0[l] - 1), J1[l]);
+                launch_mg_smooth5_residual(L, L.a, L.b, f.ctl, pass, stream);
+                const MgLevel Cl = lvl(l + 1, J0[l + 1], J1[l + 1]);
+                if (l + 1 < P) {
+                    zero(Cl);
+                    launch_mg_restrict(L, Cl, f.ctl, pass, stream);
+                    rc = mg_exchange({{l + 1, 2, kMgGhost}});
+                } else {
+                    zero(Cl);
+                    launch_mg_restrict(L, Cl, f.ctl, pass, stream);
+                    rc = mg_allgather_rhs(P);
+                }
+                if (rc) return rc;
+                launches += 3;
+            }
+            for (int l = P; l < mg_tail; ++l) {   // whole levels
+                const MgLevel L = mg[l];
+                launch_mg_smooth5_residual(L, L.a, L.b, f.ctl, pass, stream);
+                launch_mg_restrict(L, mg[l + 1], f.ctl, pass, stream);
+                launches += 2;
+            }
+            launch_mg_tail(mg_dev, mg_tail, lc, mg[mg_tail].a, mg[mg_tail].b, mg[0].fast, f.ctl, pass,
+                           stream);
+            ++launches;
+            for (int l = mg_tail - 1; l >= P; --l) {
+                const MgLevel L = mg[l], Cl = mg[l + 1];
+                launch_mg_prolong_smooth5(Cl, l + 1 == lc ? Cl.b : Cl.a, L, L.b, L.a, f.ctl, pass, stream);
+                ++launches;
+            }
+            for (int l = P - 1; l >= 0; --l) {
+                if (l + 1 < P)
+                    rc = mg_exchange({{l, 1, kSmT5}, {l + 1, 0, 3}});
+                else
+                    rc = mg_exchange({{l, 1, kSmT5}});
+                if (rc) return rc;
+                const MgLevel L = lvl(l, J0[l], J1[l]);
+                const MgLevel Cl = l + 1 < P ? lvl(l + 1, J0[l + 1], J1[l + 1]) : mg[l + 1];
+                launch_mg_prolong_smooth5(Cl, l + 1 == lc ? Cl.b : Cl.a, L, L.b, L.a, f.ctl, pass, stream);
+                ++launches;
+            }
+        }
+        // the slab's p' (and, by exchange, its deep ghosts), then the residual
+        // max |A p' - rhs| over the slab's interior rows, all-reduced
+        HIP_TRY(hipMemcpyAsync(f.pp[host_cur], mg[0].a + (long)J0[0] * nx, (size_t)g.nyl * nx * 4,
+                               hipMemcpyDeviceToDevice, stream));
+        rc = exchange_pp(host_cur, g.hg);
+        if (rc) return rc;
+        pp_ghosts_shallow = false;
+        const MgLevel L0 = lvl(0, J0[0], J1[0]);
+        launch_mg_final_residual(L0, f.pp[host_cur] - (long)J0[0] * nx, f.err_slots, f.ctl, pass, stream);
+        launch_fold_slots(f.ctl->err, f.err_slots, 1, stream);
+        rc = allreduce_max_u32(f.ctl->err, 1);
+        if (rc) return rc;
+        end_solve_timing(e0, 1, (uint64_t)launches + 1);
+        launch_finalize_solve(g, f, pass, 1, pass >= 1 ? 1 : 0, 0, stream, 1);
+        HIP_TRY(hipGetLastError());
+        if (residual_out) {
+            float r = 0.f;
+            HIP_TRY(hipMemcpyAsync(&r, &f.ctl->last_p, 4, hipMemcpyDeviceToHost, stream));
+            rc = wait_done(nullptr);
+            if (rc) return rc;
+            *residual_out = r;
+        }
+        return 0;
+    }
+    static constexpr int kSmT5 = 5;   // the smoothing window's halo (5 sweeps)
+
     int enqueue_mg(int pass, float *residual_out = nullptr) {
         int rc = mg_build();
         if (rc) return rc;
         hipEvent_t e0;
         begin_solve_timing(pass, &e0);
+        if (sharded() && mg_P > 0) return enqueue_mg_partitioned(pass, residual_out, e0);
         if (sharded()) {
             rc = gather_rhs();
             if (rc) return rc;
@@ -1037,6 +1285,21 @@ struct cfd_model {
                (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)g.nx * 4u <= (1ull << 30);
     }
 
+    // u* <- u, v* <- v and the divergence at the head of a corrector pass
+    // (model.rs:698-704): one fused launch (CFD_COPY_DIV=0: the two launches)
+    bool copy_div_env = [] {
+        const char *e = getenv("CFD_COPY_DIV");
+        return !(e && atoi(e) == 0);
+    }();
+    void pass_head(int pass, float dt_override) {
+        if (copy_div_env) {
+            launch_copy_star_div(g, f, pass, dt_override, stream);
+        } else {
+            launch_copy_star(g, f, pass, stream);
+            launch_divergence(g, f, pass, dt_override, stream);
+        }
+    }
+
     // piso_step (model.rs:529-730).
     // finish = inside update() with no extra corrector passes: the corrector,
     // the boundaries and the step reductions run as one fused pass.
@@ -1093,8 +1356,7 @@ struct cfd_model {
             if (rc) return rc;
             launch_corrector(g, f, 0, dt_override, stream);
             for (int pass = 1; pass <= params.corrector_passes; ++pass) {
-                launch_copy_star(g, f, pass, stream);
-                launch_divergence(g, f, pass, dt_override, stream);
+                pass_head(pass, dt_override);
                 rc = enqueue_solve(pass);
                 if (rc) return rc;
                 launch_corrector(g, f, pass, dt_override, stream);
@@ -1106,8 +1368,7 @@ struct cfd_model {
             if (rc) return rc;
             launch_corrector(g, f, -1, dt_override, stream);
             for (int pass = 1; pass <= params.corrector_passes; ++pass) {
-                launch_copy_star(g, f, -1, stream);
-                launch_divergence(g, f, -1, dt_override, stream);
+                pass_head(-1, dt_override);
                 rc = enqueue_solve_host_driven(&res);
                 if (rc) return rc;
                 launch_corrector(g, f, -1, dt_override, stream);

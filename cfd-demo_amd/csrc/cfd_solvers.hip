@@ -573,14 +573,14 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *
     if (win >= nwin) return;   // wave-uniform
     const int nx = L.nx, ny = L.ny;
     const int gx = (win % nwx) * kOW - kHL + lane;
-    const int gy0 = (win / nwx) * kTH - kHL;
+    const int gy0 = L.lo + (win / nwx) * kTH - kHL;   // windows tile output rows [lo, hi)
     const bool col_in = gx >= 0 && gx < nx;
     const bool bcol = gx == 0 || gx == nx - 1;
     float c[kH], rh[kH];
 #pragma unroll
     for (int y = 0; y < kH; ++y) {
         const int gy = gy0 + y;
-        const bool in = col_in && gy >= 0 && gy < ny;
+        const bool in = col_in && gy >= L.ys && gy < L.ye;
         const long k = (long)gy * nx + gx;
         c[y] = in ? (PRO ? mg_prolong_add_val(Cl, e, src[k], gx, gy) : src[k]) : 0.0f;
         rh[y] = in ? L.rhs[k] : 0.0f;
@@ -616,14 +616,14 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5w(MgLevel L, const float *
                                   L.denom * (double)c[y];
                 r = (float)((double)rh[y] - ap);
             }
-            if (out && gy < ny) L.r[(long)gy * nx + gx] = r;
+            if (out && gy < L.hi) L.r[(long)gy * nx + gx] = r;
         }
     }
     if (col_in && lane >= kHL && lane < 64 - kHL) {
 #pragma unroll
         for (int y = kHL; y < kH - kHL; ++y) {
             const int gy = gy0 + y;
-            if (gy < ny) dst[(long)gy * nx + gx] = c[y];
+            if (gy < L.hi) dst[(long)gy * nx + gx] = c[y];
         }
     }
 }
@@ -663,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5m(MgLevel L, const float *
     if (win >= nwin) return;   // wave-uniform
     const int nx = L.nx, ny = L.ny;
     const int gx = (win % nwx) * kOW - kHL + lane;
-    const int r0 = (win / nwx) * R;              // first output row
+    const int r0 = L.lo + (win / nwx) * R;       // first output row
     const int ra = r0 - kHL;                     // row of slot 0
     const bool col_in = gx >= 0 && gx < nx;
     const bool bcol = gx == 0 || gx == nx - 1;
@@ -681,7 +681,8 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5m(MgLevel L, const float *
     float RH[kMgU];
     float PQ[4];
     ProlongIn EQ[4];
-    auto rowc = [&](int u) { return min(max(ra + u, 0), ny - 1); };
+    // loads stay in the stored rows (past the grid or the slab's ghosts: clamped)
+    auto rowc = [&](int u) { return min(max(ra + u, L.ys), L.ye - 1); };
 #pragma unroll
     for (int u = 0; u < kMgPD; ++u) {
         const int gy = rowc(u);
@@ -719,7 +720,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5m(MgLevel L, const float *
             {
                 // sweep 5 of row t - 10 is final
                 const int u = t - 2 * kSmT, x = ra + u;
-                if (out && u >= kHL && u < kHL + R && x < ny)
+                if (out && u >= kHL && u < kHL + R && x < L.hi)
                     dst[(long)x * nx + gx] = W[kSmT][(j - 2 * kSmT + 64) % 4];
             }
             if (RES) {
@@ -735,7 +736,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_smooth5m(MgLevel L, const float *
                 const float r = (bcol || x <= 0 || x >= ny - 1)
                                     ? 0.0f
                                     : (float)((double)RH[(j - 2 * kSmT - 1 + 64) % kMgU] - ap);
-                if (out && u >= kHL && u < kHL + R && x < ny) L.r[(long)x * nx + gx] = r;
+                if (out && u >= kHL && u < kHL + R && x < L.hi) L.r[(long)x * nx + gx] = r;
             }
         }
     }
@@ -761,7 +762,8 @@ __global__ __launch_bounds__(kBlock) void k_mg_residual(MgLevel L, const float *
 __global__ __launch_bounds__(kBlock) void k_mg_restrict(MgLevel F, MgLevel Cl, const Ctl *ctl,
                                                         int pass, int nbx) {
     if (pass_off(ctl, pass)) return;
-    const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x, j = (int)blockIdx.x / nbx;
+    const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
+    const int j = Cl.lo + (int)blockIdx.x / nbx;   // coarse rows [lo, hi)
     if (i < Cl.nx) mg_restrict_cell(F, Cl, i, j);
 }
 
@@ -841,11 +843,11 @@ __global__ __launch_bounds__(kBlock) void k_mg_final_residual(MgLevel L, const f
     if (pass_off(ctl, pass)) return;
     __shared__ float wmax[kBlock / 64];
     const int i = ((int)blockIdx.x % nbx) * kBlock + (int)threadIdx.x;
-    const int jb = ((int)blockIdx.x / nbx) * rows;
+    const int jb = L.lo + ((int)blockIdx.x / nbx) * rows;   // rows [lo, hi)
     const int nx = L.nx;
     float m = 0.0f;
     if (i >= 1 && i <= nx - 2) {
-        const int j1 = min(jb + rows, L.ny - 1);
+        const int j1 = min(jb + rows, min(L.hi, L.ny - 1));
         for (int j = max(jb, 1); j < j1; ++j) {
             const long idx = (long)j * nx + i;
             const double r = ddiv<FAST>((double)p[idx + 1] + (double)p[idx - 1], L.dx2, L.r_dx2) +
@@ -975,7 +977,7 @@ static void launch_mg_march(const MgLevel &L, const float *src, float *dst, cons
                             const MgLevel &Cl, const float *e, hipStream_t s) {
     constexpr int kHL = kSmT + (RES ? 1 : 0);
     const int nwx = cdiv(L.nx, 64 - 2 * kHL);
-    const int nwin = nwx * cdiv(L.ny, mg_march_rows<RES>());
+    const int nwin = nwx * cdiv(L.hi - L.lo, mg_march_rows<RES>());
     const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
     if (L.fast)
         hipLaunchKernelGGL((k_mg_smooth5m<1, PRO, RES>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, Cl, e);
@@ -988,7 +990,7 @@ void launch_mg_prolong_smooth5(const MgLevel &Cl, const float *e, const MgLevel 
     if (mg_use_march(L)) return launch_mg_march<true, false>(L, src, dst, ctl, pass, Cl, e, s);
     const bool big = (long)L.nx * L.ny >= (1L << 23);
     const int nwx = cdiv(L.nx, 64 - 2 * kSmT);
-    const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+    const int nwin = nwx * cdiv(L.hi - L.lo, big ? kSmTHBig : kSmTHSmall);
     const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
 #define CFD_LAUNCH_PSM5W(FASTV, TH) \
     hipLaunchKernelGGL((k_mg_smooth5w<FASTV, TH, true>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, Cl, e)
@@ -1008,7 +1010,7 @@ void launch_mg_smooth5_residual(const MgLevel &L, const float *src, float *dst, 
     if (mg_use_march(L)) return launch_mg_march<false, true>(L, src, dst, ctl, pass, L, nullptr, s);
     const bool big = (long)L.nx * L.ny >= (1L << 23);
     const int nwx = cdiv(L.nx, 64 - 2 * (kSmT + 1));
-    const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+    const int nwin = nwx * cdiv(L.hi - L.lo, big ? kSmTHBig : kSmTHSmall);
     const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
 #define CFD_LAUNCH_RSM5W(FASTV, TH) \
     hipLaunchKernelGGL((k_mg_smooth5w<FASTV, TH, false, true>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, L, nullptr)
@@ -1030,7 +1032,7 @@ void launch_mg_smooth5(const MgLevel &L, const float *src, float *dst, const Ctl
     if (mg_smooth_wave_form()) {
         const bool big = (long)L.nx * L.ny >= (1L << 23);
         const int nwx = cdiv(L.nx, 64 - 2 * kSmT);
-        const int nwin = nwx * cdiv(L.ny, big ? kSmTHBig : kSmTHSmall);
+        const int nwin = nwx * cdiv(L.hi - L.lo, big ? kSmTHBig : kSmTHSmall);
         const dim3 grid(cdiv(nwin, kBlock / 64)), block(kBlock);
 #define CFD_LAUNCH_SM5W(FASTV, TH) \
         hipLaunchKernelGGL((k_mg_smooth5w<FASTV, TH, false>), grid, block, 0, s, L, src, dst, ctl, pass, nwx, nwin, L, nullptr)
@@ -1069,8 +1071,9 @@ void launch_mg_residual(const MgLevel &L, const float *p, const Ctl *ctl, int pa
 }
 
 void launch_mg_restrict(const MgLevel &F, const MgLevel &Cl, const Ctl *ctl, int pass, hipStream_t s) {
+    if (Cl.hi <= Cl.lo) return;
     int nbx;
-    const int g = grid_of(Cl.nx, Cl.ny, &nbx);
+    const int g = grid_of(Cl.nx, Cl.hi - Cl.lo, &nbx);
     hipLaunchKernelGGL(k_mg_restrict, dim3(g), dim3(kBlock), 0, s, F, Cl, ctl, pass, nbx);
 }
 
@@ -1095,12 +1098,13 @@ void launch_mg_final_residual(const MgLevel &L, const float *p, uint32_t *slots,
                               int pass, hipStream_t s) {
     const int nbx = cdiv(L.nx, kBlock);
     const int rows = 32;
+    const dim3 grid(nbx * std::max(1, cdiv(L.hi - L.lo, rows)));
     if (L.fast)
-        hipLaunchKernelGGL(k_mg_final_residual<1>, dim3(nbx * cdiv(L.ny, rows)), dim3(kBlock), 0, s,
-                           L, p, slots, ctl, pass, nbx, rows);
+        hipLaunchKernelGGL(k_mg_final_residual<1>, grid, dim3(kBlock), 0, s, L, p, slots, ctl, pass,
+                           nbx, rows);
     else
-        hipLaunchKernelGGL(k_mg_final_residual<0>, dim3(nbx * cdiv(L.ny, rows)), dim3(kBlock), 0, s,
-                           L, p, slots, ctl, pass, nbx, rows);
+        hipLaunchKernelGGL(k_mg_final_residual<0>, grid, dim3(kBlock), 0, s, L, p, slots, ctl, pass,
+                           nbx, rows);
 }
 
 }  // namespace cfd

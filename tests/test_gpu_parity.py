@@ -353,7 +353,7 @@ def test_power_of_two_cavity_uses_reciprocal_multiply():
     m = c.Model(c.cavity_grid(4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
                                                                tol_enabled=False))
     assert m.kernel_config == {"fastdiv": 1, "temporal": 8}
-    assert m.jacobi_kernel == {"kind": 5, "name": "k_jacobi_lds<8, 1, false>"}
+    assert m.jacobi_kernel == {"kind": 5, "name": "k_jacobi_lds<8, 1, 0>"}
 
 
 def test_kernel_selection_rules(monkeypatch):

@@ -372,3 +372,24 @@ def test_sharded_full_size_developed_across_boundaries(n, nx, ny):
         got1 = assemble(one, nx)
         for f in FIELDS + ("rhs",):
             assert_bitwise(f"{f} (2 slabs, 1 developed step) vs oracle", got1[f], o.field(f))
+
+
+@pytest.mark.parametrize("n,nx,ny,tol,part", [(4, 512, 512, False, "1"), (2, 512, 384, True, "1"),
+                                              (3, 384, 192, False, "1"), (4, 512, 512, False, "0")])
+def test_sharded_multigrid_partitioned_levels(monkeypatch, n, nx, ny, tol, part):
+    """Multigrid on slabs with the fine levels partitioned (each rank smooths,
+    restricts and prolongs its own rows of levels 0..P-1, with ghost-row
+    exchanges; the coarse levels are gathered whole): 512^2 on 4 slabs
+    partitions levels 0-2 (level 3 = the tail's), 512x384 on 2 slabs levels
+    0-2, 384x192 on 3 slabs levels 0-1; CFD_MG_PARTITION=0 keeps the
+    whole-grid-per-rank form.  Bitwise against the single-domain oracle, with
+    corrector passes, tolerance off and on."""
+    import cfdamd
+    monkeypatch.setenv("CFD_MG_PARTITION", part)
+    grid = cfdamd.cavity_grid(nx, ny)
+    params = cfdamd.SimulationParams.cavity(400.0, 50, pressure_solver=cfdamd.PressureSolver.Multigrid,
+                                            corrector_passes=2, tol_enabled=tol)
+    st = run_sharded(n, grid, params, 3, 4)
+    check_against_oracle(st, grid, dict(bc_kind=1, viscosity=1.0 / 400.0, pressure_solver=2,
+                                        corrector_passes=2, tol_enabled=int(tol)), 3,
+                         FIELDS + ("rhs",))

@@ -122,3 +122,21 @@ def test_spec_off_matches_spec_on(monkeypatch):
     for f in STATE:
         assert_bitwise(f"spec on/off:{f}", states[1][f], states[0][f])
     assert states[0]["jacobi_sweeps_total"] == states[1]["jacobi_sweeps_total"]
+
+
+def test_fused_pass_head_matches_two_launches(monkeypatch):
+    """The corrector-pass head fused into one launch (k_copy_star_div) and the
+    two launches it replaces (CFD_COPY_DIV=0) give the same bits, with passes
+    running (tolerance on, channel with a cylinder)."""
+    import cfdamd
+    grid = cfdamd.Grid(256, 96, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5))
+    params = cfdamd.SimulationParams(jacobi_iters=30, corrector_passes=6)
+    states = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("CFD_COPY_DIV", env)
+        m = cfdamd.Model(grid, params, device=0)
+        m.update_n(12)
+        states.append(m.get_state())
+        m.close()
+    for f in STATE:
+        assert_bitwise(f"pass head fused/unfused:{f}", states[1][f], states[0][f])
