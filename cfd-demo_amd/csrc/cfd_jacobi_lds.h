@@ -231,11 +231,24 @@ struct LdsMarch {
             const f2 &Tp = W[s - 1][(V_ - dl + kW) % NW];            //            row r+1
             if (REDO && s > nst) continue;                            // wave-uniform
             f2 n = stage<E>(B, C, Tp, rh);
-            if (SPEC && r >= r0v && r < r1v) {
-                // every stage is one reference sweep: its max |new - old| over
-                // the segment's own rows (each row counted by one segment)
-                const int ra = act(r);
-                if (ra >= 0 && ra < nyl_) {
+            if constexpr (SPEC) {
+                // every stage is one reference sweep: its max |new - old|.
+                // Waves whose rows reach no global boundary row take every
+                // row they compute, branch-free: a row outside the segment
+                // [r0v, r1v) (warm-up and run-out cone) holds the exact
+                // sweep value of an interior row — its inputs are all loaded
+                // rows, k_first = r0v - T — which the segment owning it also
+                // counts, and a max is unchanged by a repeated element.  The
+                // row-edge waves count only their own rows: with k_first =
+                // r0v - T, r - r0v = v - s - T (compile-time in the warm-up).
+                bool in_seg;
+                if constexpr (!(E & kRow))
+                    in_seg = true;
+                else if constexpr (GUARD == 0)
+                    in_seg = V_ - s - T >= 0 && v - s - T < r1v - r0v;
+                else
+                    in_seg = v - s - T >= 0 && v - s - T < r1v - r0v;
+                if (in_seg) {
                     const f2 d = n - C;
                     if (!(E & kCol)) {
                         mm[s - 1] = fmaxf(fmaxf(mm[s - 1], fabsf(d.x)), fabsf(d.y));
@@ -350,13 +363,17 @@ struct LdsMarch {
     }
 };
 
-#if CFD_LDS_WPE > 0
-#define CFD_LDS_BOUNDS __launch_bounds__(kLdsWaves * 64, CFD_LDS_WPE)
-#else
-#define CFD_LDS_BOUNDS __launch_bounds__(kLdsWaves * 64)
+// Minimum waves per SIMD the register allocation must allow (the SPEC
+// launch holds T residual maxima on top of the plain march: 99 VGPRs, 4
+// waves; pinned to 5 it spills).
+#ifndef CFD_LDS_SPEC_WPE
+#define CFD_LDS_SPEC_WPE 5
 #endif
+constexpr int lds_min_waves(int mode) {
+    return mode == 2 ? CFD_LDS_SPEC_WPE : (CFD_LDS_WPE > 0 ? CFD_LDS_WPE : 1);
+}
 template <int T, int FAST, int MODE>
-__global__ CFD_LDS_BOUNDS void k_jacobi_lds(
+__global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
     int wlo, int whi) {

@@ -39,12 +39,18 @@ inline void plan_sweep(int j0, int nyl, int ny, int hg, int it, int iters, int *
 // *T = min(t_max, sweeps left before the next exchange, sweeps left in the
 // solve) sweeps in one launch and stores its final sweep on local rows
 // [out_lo, out_hi) (= what plan_sweep gives for the block's last sweep);
-// *exchange as in plan_sweep.  hg <= 0 means unsharded (no exchanges).
+// *exchange as in plan_sweep.  hg <= 0 means unsharded (no exchanges): then
+// the solve's ceil(iters / t_max) launches share its sweeps evenly.
 inline void plan_block(int j0, int nyl, int ny, int hg, int it, int t_max, int iters, int *T,
                        int *out_lo, int *out_hi, int *exchange) {
     const int lo_g = 1 - j0, hi_g = ny - 1 - j0;
     if (hg <= 0) {
-        *T = std::min(t_max, iters - it);
+        // the same number of launches as t_max-sized blocks, the sweeps
+        // spread evenly over them (50 = 8 + 6 x 7, not 6 x 8 + 2): a short
+        // tail launch costs a whole pass over p' and rhs for few sweeps
+        const int rem = iters - it, t = std::max(1, t_max);
+        const int nl = (rem + t - 1) / t;
+        *T = nl > 0 ? (rem + nl - 1) / nl : 0;
         *out_lo = lo_g;
         *out_hi = hi_g;
         *exchange = 0;

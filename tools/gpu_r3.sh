@@ -27,6 +27,22 @@ for s in $STEPS; do
       export TMPDIR=/tmp
       step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- \
         python3 bench.py --no-cpu-baseline --no-control --no-parity --no-so --no-parity-mode ;;
+    parity)
+      # the reference's control flow (tolerance on) under the kernel tracer, C3 and C2
+      export TMPDIR=/tmp
+      step parity4096 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o parity4096 --output-format csv -- \
+        python3 tools/parity_one.py 4096 3
+      step parity1024 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o parity1024 --output-format csv -- \
+        python3 tools/parity_one.py 1024 5 ;;
+    cputable) step cputable 600 python3 tools/cpu_table.py --budget 15 ;;
+    rehearse)
+      # exactly as the driver invokes it (no external launcher); loopback puts
+      # every rank on this box's one GPU (RCCL socket transport)
+      step rehearse_n2 300 env CFD_BENCH_LOOPBACK=1 python3 bench.py --gpus 2
+      step rehearse_n4 300 env CFD_BENCH_LOOPBACK=1 python3 bench.py --gpus 4
+      # without loopback a 1-GPU box must refuse --gpus 2 (never an n_gpus 1 line)
+      timeout -k 10 120 python3 bench.py --gpus 2 > gpurun_out/${TAG}_refuse_n2.log 2>&1
+      echo "refuse_n2 rc=$?" | tee -a gpurun_out/${TAG}_refuse_n2.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
