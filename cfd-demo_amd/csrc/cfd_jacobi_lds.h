@@ -512,17 +512,40 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 
 // Workgroups of k_jacobi_lds<T, FAST, RES> one CU holds at once (occupancy
 // API, cached per instantiation).
+// Dynamic LDS added to a launch (bytes) to cap the workgroups the hardware
+// places on one CU, so a round of resident waves is spread evenly at a chosen
+// occupancy.  Default: 24 KiB on fixed-count launches (MODE 0/1) whose p'
+// pair + rhs fit the 256 MiB Infinity Cache: 18 + 24 KiB per 4-wave
+// workgroup admits 3 per CU (3 waves per SIMD) where the registers allow 5,
+// and the round's 3/5 of the waves each march a 5/3 longer segment (less
+// warm-up recompute) on a launch that is VALU- not memory-bound: developed
+// 4096^2 cavity 5.60 -> 5.28 us/sweep (profiles/r3/ab_pad3.log).  None on
+// HBM-streaming slabs, where more waves in flight pay (8192^2: 23.8 vs 24.5
+// us/sweep padded), nor on the speculative launches (ab_pad_parity.log).
+// CFD_LDS_PAD=<bytes> forces one value on every launch.
+inline int lds_pad_bytes(const Geom &g, int mode) {
+    static const int forced = [] {
+        const char *e = getenv("CFD_LDS_PAD");
+        return e ? std::max(0, std::min(64 * 1024, atoi(e))) : -1;
+    }();
+    if (forced >= 0) return forced;
+    constexpr uint64_t kMallResident = 200ull << 20;
+    const uint64_t ws = 3ull * (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)g.nx * 4u;
+    return mode <= 1 && ws <= kMallResident ? 24 * 1024 : 0;
+}
 template <int T, int FAST, int MODE>
-int lds_blocks_per_cu() {
-    static const int nb = [] {
+int lds_blocks_per_cu(int pad) {
+    static int cache[2] = {0, 0};   // unpadded, padded (one pad value per process)
+    int &nb = cache[pad > 0 ? 1 : 0];
+    if (nb == 0) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &n, reinterpret_cast<const void *>(&k_jacobi_lds<T, FAST, MODE>), kLdsWaves * 64, 0) !=
+                &n, reinterpret_cast<const void *>(&k_jacobi_lds<T, FAST, MODE>), kLdsWaves * 64, pad) !=
                 hipSuccess ||
             n < 1)
             n = 1;
-        return n;
-    }();
+        nb = n;
+    }
     return nb;
 }
 
@@ -532,10 +555,18 @@ int lds_blocks_per_cu() {
 // second, partial round — or whole multiples of a round when a round would
 // make segments longer than kMaxRows.
 template <int T, int FAST, int MODE>
-int lds_segments(const Geom &g, int nrows, int nwc) {
+int lds_segments(const Geom &g, int nrows, int nwc, int pad) {
     if (g.tb_rows > 0) return cdiv(nrows, g.tb_rows);
     constexpr int kMaxRows = 160, kMinRows = 8;
-    const int wgs_per_col = std::max(1, g.n_cu * lds_blocks_per_cu<T, FAST, MODE>() / nwc);
+    // CFD_LDS_BPC caps the workgroups per CU a round is sized for (below the
+    // occupancy limit: fewer, longer segments, less warm-up recompute)
+    static const int bpc_cap = [] {
+        const char *e = getenv("CFD_LDS_BPC");
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
+    const int occ = lds_blocks_per_cu<T, FAST, MODE>(pad);
+    const int bpc = bpc_cap > 0 ? std::min(occ, bpc_cap) : occ;
+    const int wgs_per_col = std::max(1, g.n_cu * bpc / nwc);
     const int per_round = kLdsWaves * wgs_per_col;
     const int rounds = std::max(1, cdiv(nrows, (long)per_round * kMaxRows));
     return std::max(1, std::min(per_round * rounds, nrows / kMinRows));
@@ -547,9 +578,10 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo,
     const int nch = g.nx / 2;
     const int nwc = cdiv(nch, LdsMarch<T, 1, MODE>::OUTL);
     const int nrows = out_hi - out_lo;
-    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, MODE>(g, nrows, nwc)
-                     : g.fastdiv == 2 ? lds_segments<T, 2, MODE>(g, nrows, nwc)
-                                      : lds_segments<T, 0, MODE>(g, nrows, nwc);
+    const int pad = lds_pad_bytes(g, MODE);
+    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, MODE>(g, nrows, nwc, pad)
+                     : g.fastdiv == 2 ? lds_segments<T, 2, MODE>(g, nrows, nwc, pad)
+                                      : lds_segments<T, 0, MODE>(g, nrows, nwc, pad);
     const dim3 grid(nwc * cdiv(nseg, kLdsWaves)), block(kLdsWaves * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     // a segment whose rows reach a global boundary row runs the kCol|kRow
@@ -560,7 +592,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo,
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
-    hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, 0, s, g, pa, pb, f.rhs, f.ctl, \
+    hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
                        rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);

@@ -807,6 +807,64 @@ __global__ __launch_bounds__(kBlock) void k_corrector(Geom g, Fields f, int pass
     }
 }
 
+// k_corrector with a thread per 4 consecutive cells of a row: the p', v, v*
+// and p rows (pitch nx, 16-byte aligned) move as float4, the u / u* row
+// (pitch nx+1) as scalars; the left neighbour p'(i0-1) of the first u face is
+// one more scalar load.  The same expressions per face and cell as
+// k_corrector (Q9 tail included), so the same bits; one float per thread held
+// the corrector at ~4 TB/s.
+template <int SP>
+__global__ __launch_bounds__(kBlock) void k_corrector4(Geom g, Fields f, int pass,
+                                                       float dt_override, int nbx) {
+    Ctl *c = f.ctl;
+    if (pass_off(c, pass)) return;
+    const int bid = xcd_block(g);
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);   // cells i0..i0+3
+    const int lj = bid / nbx;                                       // 0..nyl
+    const int nx = g.nx, W = nx + 1;
+    if (i0 >= nx) return;
+    const float dt = dt_of(c, dt_override);
+    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+    const int j = g.j0 + lj;
+    const long kc = (long)lj * nx + i0;
+    float4 pc = {0.f, 0.f, 0.f, 0.f};
+    if (lj < g.nyl) {
+        pc = *reinterpret_cast<const float4 *>(pp + kc);
+        const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
+        const float pr[4] = {pc.x, pc.y, pc.z, pc.w};
+        const float pw[4] = {pl, pc.x, pc.y, pc.z};
+        const long ku = (long)lj * W + i0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = i0 + q;
+            if (i < 1 || i > nx - 1) continue;
+            if (i >= nx - 7)
+                f.u[ku + q] = f.u_star[ku + q] - sdiv<SP>(dt * (pr[q] - pw[q]), g.dx, g.r_dx);
+            else
+                f.u[ku + q] = f.u_star[ku + q] - dt * sdiv<SP>(pr[q] - pw[q], g.dx, g.r_dx);
+        }
+    }
+    if (j >= 1 && j <= g.ny - 1) {
+        const float4 pt = lj < g.nyl ? pc : *reinterpret_cast<const float4 *>(pp + kc);
+        const float4 pb = *reinterpret_cast<const float4 *>(pp + kc - nx);
+        const float4 vs = *reinterpret_cast<const float4 *>(f.v_star + kc);
+        float4 o;
+        o.x = vs.x - dt * sdiv<SP>(pt.x - pb.x, g.dy, g.r_dy);
+        o.y = vs.y - dt * sdiv<SP>(pt.y - pb.y, g.dy, g.r_dy);
+        o.z = vs.z - dt * sdiv<SP>(pt.z - pb.z, g.dy, g.r_dy);
+        o.w = vs.w - dt * sdiv<SP>(pt.w - pb.w, g.dy, g.r_dy);
+        *reinterpret_cast<float4 *>(f.v + kc) = o;
+    }
+    if (lj < g.nyl) {
+        float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
+        pv.x = pv.x + pc.x;
+        pv.y = pv.y + pc.y;
+        pv.z = pv.z + pc.z;
+        pv.w = pv.w + pc.w;
+        *reinterpret_cast<float4 *>(f.p + kc) = pv;
+    }
+}
+
 // ------------------------------------------------- velocity boundaries (K6)
 
 // Inlet face value of row j (model.rs:830-846): uniform or parabolic, >= 0.
@@ -1501,6 +1559,20 @@ void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, 
 
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s) {
+    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    const char *ve = getenv("CFD_CORR_VEC");   // 0: the one-float-per-thread kernel
+    const bool vec_env = !(ve && atoi(ve) == 0);
+    if (vec_env && g.nx % 4 == 0 && a16(f.v) && a16(f.v_star) && a16(f.p) && a16(f.pp[0]) &&
+        a16(f.pp[1])) {
+        const int nbx4 = cdiv(g.nx / 4, kBlock);
+        if (g.sp_pow2)
+            hipLaunchKernelGGL(k_corrector4<1>, dim3(nbx4 * (g.nyl + 1)), dim3(kBlock), 0, s, g, f,
+                               pass, dt_override, nbx4);
+        else
+            hipLaunchKernelGGL(k_corrector4<0>, dim3(nbx4 * (g.nyl + 1)), dim3(kBlock), 0, s, g, f,
+                               pass, dt_override, nbx4);
+        return;
+    }
     const int nbx = cdiv(g.nx + 1, kBlock);
     if (g.sp_pow2)
         hipLaunchKernelGGL(k_corrector<1>, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,

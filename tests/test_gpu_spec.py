@@ -140,3 +140,26 @@ def test_fused_pass_head_matches_two_launches(monkeypatch):
         m.close()
     for f in STATE:
         assert_bitwise(f"pass head fused/unfused:{f}", states[1][f], states[0][f])
+
+
+@pytest.mark.parametrize("grid_kind", ["channel", "cavity"])
+def test_vector_corrector_matches_scalar(monkeypatch, grid_kind):
+    """The corrector passes' 4-cells-per-thread kernel (k_corrector4) and the
+    one-float-per-thread k_corrector (CFD_CORR_VEC=0) give the same bits with
+    passes running: u faces incl. the Q9 tail, v faces, p += p'."""
+    import cfdamd
+    if grid_kind == "channel":
+        grid = cfdamd.Grid(256, 96, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5))
+        params = cfdamd.SimulationParams(jacobi_iters=30, corrector_passes=6)
+    else:
+        grid = cfdamd.cavity_grid(192, 128)
+        params = cfdamd.SimulationParams.cavity(400.0, 50, p_tol=2e-4)
+    states = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("CFD_CORR_VEC", env)
+        m = cfdamd.Model(grid, params, device=0)
+        m.update_n(10)
+        states.append(m.get_state())
+        m.close()
+    for f in STATE:
+        assert_bitwise(f"corrector vec/scalar {grid_kind}:{f}", states[1][f], states[0][f])
