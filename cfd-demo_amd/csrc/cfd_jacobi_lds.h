@@ -68,6 +68,10 @@ constexpr int kStampWaves = 1 << 15;
 __device__ unsigned long long g_lds_stamp[kStampWaves * 4];
 #endif
 
+#ifndef CFD_LDS_ST_AUX
+#define CFD_LDS_ST_AUX 16  // p' stores write-through (sc1): 5.07 vs 5.13 us/sweep plain, nt 5.78 (r3 ab_staux.log)
+#endif
+
 #ifndef CFD_LDS_HOIST
 #define CFD_LDS_HOIST 0  // 1: read a slot's T rhs rows from the LDS ring at its start (r2: 5.09 vs 5.00 us/sweep, off)
 #endif
@@ -157,7 +161,7 @@ struct LdsMarch {
     }
     __device__ __forceinline__ void st(const f2 &x, int row) const {
         const u32x2 v = {__float_as_uint(x.x), __float_as_uint(x.y)};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - lo_clamp) * row_bytes, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - lo_clamp) * row_bytes, CFD_LDS_ST_AUX);
     }
 
     // One reference update (model.rs:775-793) of the lane's column pair.
