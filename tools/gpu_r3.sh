@@ -25,7 +25,7 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)
       export TMPDIR=/tmp
-      step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- \
+      step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
         python3 bench.py --no-cpu-baseline --no-control --no-parity --no-so --no-parity-mode ;;
     parity)
       # the reference's control flow (tolerance on) under the kernel tracer, C3 and C2
