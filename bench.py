@@ -454,6 +454,7 @@ def main():
         # trick): every rank on device 0, each its own RCCL "host" so RCCL
         # connects them through its socket transport; set before RCCL loads
         os.environ["NCCL_HOSTID"] = f"cfd-bench-rank{rank}"
+        os.environ["CFD_PERSIST"] = "0"   # ranks share the GPU (persistent solves need it whole)
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
         os.environ.setdefault("NCCL_NET", "Socket")

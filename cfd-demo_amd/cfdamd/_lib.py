@@ -78,7 +78,7 @@ class CfdAabb(C.Structure):
 
 
 # cfd_status (include/cfd.h)
-CFD_EINVAL, CFD_EHIP, CFD_ERCCL, CFD_ESTATE, CFD_ENONFINITE = -1, -2, -3, -4, -5
+CFD_EINVAL, CFD_EHIP, CFD_ERCCL, CFD_ESTATE, CFD_ENONFINITE, CFD_ETIMEOUT = -1, -2, -3, -4, -5, -6
 
 
 class CfdError(RuntimeError):

@@ -35,7 +35,12 @@ constexpr int kMaxPasses = 64;     // corrector passes + 1
 // the 4 step maxima own red_slots likewise.  Slots are zero between uses.
 constexpr int kResSlots = 32;
 constexpr int kResStride = 16;
-constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 8) * kResSlots * kResStride;
+// persistent-solve words (k_jacobi_persist): [1] timeout flag, then one
+// hand-off flag per workgroup on a 64-B line of its own
+constexpr int kPersistFlagStride = 16;
+constexpr int kPersistMaxGroups = 4096;
+constexpr size_t kPersistWords = (size_t)(kPersistMaxGroups + 1) * kPersistFlagStride;
+constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 8) * kResSlots * kResStride + kPersistWords;
 
 // Device-resident control block: every data-dependent decision of
 // Model::update lives here so a whole step can be enqueued (or replayed as a
@@ -122,6 +127,7 @@ struct Fields {
     // host-mapped word the step finalize sets to Ctl::step (sharded models):
     // the RCCL watchdog's evidence of forward progress
     uint32_t *host_progress;
+    uint32_t *persist;   // kPersistWords words after the slot sets (see kPersistFlagStride)
 };
 
 // ---- launchers (cfd_kernels.hip) ----
@@ -163,6 +169,12 @@ void launch_jacobi_sweep(const Geom &g, const Fields &f, int pass, int it, int r
 // buffers flip once per launch).
 void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int par, int T,
                          int out_lo, int out_hi, int res, hipStream_t s);
+// nblk consecutive 8-sweep kind-5 blocks (no residual) in ONE persistent
+// launch whose workgroups hand rows to their neighbours through flags
+// (k_jacobi_persist); returns false (nothing launched) where the one-round
+// geometry does not apply
+bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,
+                           int out_lo, int out_hi, uint32_t epoch, hipStream_t s);
 // The block kernels behind it: k_jacobi_tb (T <= 4, cfd_jacobi_tb1.hip) and
 // the prefetch-pipelined march with 4 or 2 columns per lane (T <= 8,
 // cfd_jacobi_pipe4.hip / cfd_jacobi_pipe2.hip).
@@ -175,6 +187,8 @@ void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int p
                   int out_hi, uint32_t *res_slots, hipStream_t s);
 // kind 5: the same march with its rhs window in LDS (cfd_jacobi_lds.hip, T <= 8);
 // mode 2 / 3: the speculative launch / its re-run (launch_jacobi_spec)
+bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
+                         int out_hi, uint32_t epoch, hipStream_t s);
 void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
                 int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0);
 // Speculative temporal blocking for the tolerance mode (model.rs:748-819):

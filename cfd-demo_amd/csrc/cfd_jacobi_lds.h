@@ -72,6 +72,10 @@ __device__ unsigned long long g_lds_stamp[kStampWaves * 4];
 #define CFD_LDS_ST_AUX 16  // p' stores write-through (sc1): 5.07 vs 5.13 us/sweep plain, nt 5.78 (r3 ab_staux.log)
 #endif
 
+#ifndef CFD_LDS_LD_AUX
+#define CFD_LDS_LD_AUX 0  // cache-policy bits of the p' loads (16 = sc1: bypass L1)
+#endif
+
 #ifndef CFD_LDS_HOIST
 #define CFD_LDS_HOIST 0  // 1: read a slot's T rhs rows from the LDS ring at its start (r2: 5.09 vs 5.00 us/sweep, off)
 #endif
@@ -104,6 +108,12 @@ constexpr int ring_depth(int T, int PD, int G) {
 template <int T, int FAST, int MODE>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1, SPEC = MODE == 2, REDO = MODE == 3;
+    // MODE 4 (PERSIST): a block of k_jacobi_persist; p' moves between
+    // workgroups inside the launch, so its loads bypass L1 and its stores
+    // write through (sc1 both ways, MI355X_MICROARCH.md visibility rules)
+    static constexpr bool PERSIST = MODE == 4;
+    static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
+    static constexpr int PST_AUX = PERSIST ? 16 : CFD_LDS_ST_AUX;
     // Stage s of slot v computes row k - s - off(s).  With G = 1 (off = 0)
     // this is the plain pipeline: stage s reads stage s-1's row of the SAME
     // slot, one serial chain of T dependent updates per slot.  With G > 1 the
@@ -138,7 +148,10 @@ struct LdsMarch {
     int k_first, S, lo_clamp, hi_clamp, nch, g_first, g_last, g_top, g_zero, row_bytes;
     int ch, vo_ld, vo_st, abase, dir;
     bool e0, e1;         // residual columns (kCol slots)
-    const Geom *g;       // the kernel argument: divisors and their reciprocals
+    // the Jacobi divisors and their reciprocals (uniform values, not a pointer
+    // to the kernel argument: a pointer escaping into the block function made
+    // the compiler copy the argument to scratch)
+    float dx_sq, r_dx_sq, dy_sq, r_dy_sq, denom, r_denom;
     __amdgpu_buffer_rsrc_t rs_p, rs_r, rs_d;
     float m;
     float mm[SPEC ? T : 1];   // SPEC: stage s's residual (segment rows only)
@@ -151,17 +164,18 @@ struct LdsMarch {
     // allocation lie beyond the global boundary and rows past the segment's
     // last input row are never needed: both are clamped to a row that exists
     // (their values only reach halo rows that the boundary patch overwrites).
+    template <int AUX = 0>
     __device__ __forceinline__ f2 ld(__amdgpu_buffer_rsrc_t rs, int vrow) const {
         if (CFD_LDS_DIAG & 1) return (f2){__int_as_float(vo_ld + vrow), 1.0f};
         vrow = vrow < k_first + S ? vrow : k_first + S - 1;
         int row = act(vrow);
         row = row < lo_clamp ? lo_clamp : (row > hi_clamp ? hi_clamp : row);
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo_ld, (row - lo_clamp) * row_bytes, 0);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo_ld, (row - lo_clamp) * row_bytes, AUX);
         return (f2){__uint_as_float(v.x), __uint_as_float(v.y)};
     }
     __device__ __forceinline__ void st(const f2 &x, int row) const {
         const u32x2 v = {__float_as_uint(x.x), __float_as_uint(x.y)};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - lo_clamp) * row_bytes, CFD_LDS_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - lo_clamp) * row_bytes, PST_AUX);
     }
 
     // One reference update (model.rs:775-793) of the lane's column pair.
@@ -172,9 +186,9 @@ struct LdsMarch {
         const float hy = C.x + from_right(C.x);
         const f2 h = {hx, hy};
         const f2 v = Tp + B;
-        const f2 hz = fdiv2<FAST>(h, g->dx_sq, g->r_dx_sq);
-        const f2 vt = fdiv2<FAST>(v, g->dy_sq, g->r_dy_sq);
-        const f2 pu = fdiv2<FAST>(hz + vt - Rh, g->denom, g->r_denom);
+        const f2 hz = fdiv2<FAST>(h, dx_sq, r_dx_sq);
+        const f2 vt = fdiv2<FAST>(v, dy_sq, r_dy_sq);
+        const f2 pu = fdiv2<FAST>(hz + vt - Rh, denom, r_denom);
         const float omega = 0.75f;
         const float om1 = 1.0f - omega;
         return omega * pu + om1 * C;
@@ -205,7 +219,7 @@ struct LdsMarch {
         if (CFD_LDS_SB >= 1) __builtin_amdgcn_sched_barrier(0);
         const int k = k_first + v;
         W[0][V_ % NW] = PQ[V_ % PD];                                 // input row k
-        PQ[V_ % PD] = ld(rs_p, k + PD);
+        PQ[V_ % PD] = ld<PLD_AUX>(rs_p, k + PD);
         if (!(CFD_LDS_DIAG & 2))
             ring[(V_ % D) * 64 + lane] = RQ[V_ % PD];                 // rhs row k
         RQ[V_ % PD] = ld(rs_r, k + PD);
@@ -367,56 +381,22 @@ struct LdsMarch {
     }
 };
 
-// Minimum waves per SIMD the register allocation must allow (the SPEC
-// launch holds T residual maxima on top of the plain march: 99 VGPRs, 4
-// waves; pinned to 5 it spills).
-#ifndef CFD_LDS_SPEC_WPE
-#define CFD_LDS_SPEC_WPE 5
-#endif
-constexpr int lds_min_waves(int mode) {
-    return mode == 2 ? CFD_LDS_SPEC_WPE : (CFD_LDS_WPE > 0 ? CFD_LDS_WPE : 1);
-}
+// One T-sweep block of one workgroup's four wave tiles (the body of
+// k_jacobi_lds; k_jacobi_persist runs it once per block).  `bid`: the
+// workgroup's (XCD-renumbered) index.  Returns without touching memory for
+// waves with no rows.
 template <int T, int FAST, int MODE>
-__global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
-    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
-    int wlo, int whi) {
+__device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
+                                          float *__restrict__ pb, const float *__restrict__ rhs,
+                                          Ctl *ctl, uint32_t *res_slots, int par, int out_lo,
+                                          int out_hi, int nwc, int nseg, int wlo, int whi, f2 *lds,
+                                          int nst, int bid) {
     using M = LdsMarch<T, FAST, MODE>;
     constexpr bool RES = M::RES;
-    __shared__ f2 lds[kLdsWaves * M::D * 64];
-#if CFD_LDS_STAMP
-    const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
-    struct StampOnExit {
-        unsigned long long rt0, t0;
-        __device__ ~StampOnExit() {
-            if (RES) return;
-            const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
-            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-            // hwreg(id, 0, 32): HW_ID = 4, XCC_ID = 20
-            const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
-            const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
-            const int idx = (int)blockIdx.x * kLdsWaves + ((int)threadIdx.x >> 6);
-            if ((threadIdx.x & 63) == 0 && idx < kStampWaves) {
-                g_lds_stamp[idx * 4 + 0] = rt0;
-                g_lds_stamp[idx * 4 + 1] = rt1;
-                g_lds_stamp[idx * 4 + 2] = t1 - t0;
-                g_lds_stamp[idx * 4 + 3] = ((unsigned long long)xcc << 32) | hw;
-            }
-        }
-    } stamp_guard{st_rt0, st_t0};
-#endif
-    if (pass_off(ctl, pass)) return;
-    if (M::SPEC && ctl->spec_stop) return;   // an earlier launch of the solve converged
     M w;
-    if (M::REDO) {
-        w.nst = ctl->spec_redo;
-        if (w.nst <= 0) return;
-        par = ctl->spec_launch;   // re-run that launch: same source, same destination
-    }
+    w.nst = nst;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int lane = (int)threadIdx.x & 63;
-    const int bid = xcd_block(g);
     const int wc = bid % nwc;
     const int seg = (bid / nwc) * kLdsWaves + wave;
     const int nrows = out_hi - out_lo;
@@ -452,7 +432,12 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
     w.rs_d = __builtin_amdgcn_make_buffer_rsrc(dst_alloc, 0, pbytes, 0x00020000);
     w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)g.hg * nx), 0, pbytes,
                                                0x00020000);
-    w.g = &g;
+    w.dx_sq = g.dx_sq;
+    w.r_dx_sq = g.r_dx_sq;
+    w.dy_sq = g.dy_sq;
+    w.r_dy_sq = g.r_dy_sq;
+    w.denom = g.denom;
+    w.r_denom = g.r_denom;
     // residual columns 1..=nx-8 (the reference's full 8-lane chunks, Q6)
     w.e0 = out_lane && col >= 1 && col <= nx - 8;
     w.e1 = out_lane && col + 1 >= 1 && col + 1 <= nx - 8;
@@ -492,7 +477,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
     }
 #pragma unroll
     for (int q = 0; q < M::PD; ++q) {
-        w.PQ[q] = w.ld(w.rs_p, w.k_first + q);
+        w.PQ[q] = w.template ld<M::PLD_AUX>(w.rs_p, w.k_first + q);
         w.RQ[q] = w.ld(w.rs_r, w.k_first + q);
     }
     if (row_edge)
@@ -512,6 +497,139 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
     if (!RES) return;
     const float m = wave_max(out_lane ? w.m : 0.0f);
     if (lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, m);
+}
+
+// Minimum waves per SIMD the register allocation must allow (the SPEC
+// launch holds T residual maxima on top of the plain march: 99 VGPRs, 4
+// waves; pinned to 5 it spills).
+#ifndef CFD_LDS_SPEC_WPE
+#define CFD_LDS_SPEC_WPE 5
+#endif
+constexpr int lds_min_waves(int mode) {
+    return mode == 2 ? CFD_LDS_SPEC_WPE : (CFD_LDS_WPE > 0 ? CFD_LDS_WPE : 1);
+}
+template <int T, int FAST, int MODE>
+__global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
+    int wlo, int whi) {
+    using M = LdsMarch<T, FAST, MODE>;
+    [[maybe_unused]] constexpr bool RES = M::RES;   // the stamp guard's
+    __shared__ f2 lds[kLdsWaves * M::D * 64];
+#if CFD_LDS_STAMP
+    const unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+    struct StampOnExit {
+        unsigned long long rt0, t0;
+        __device__ ~StampOnExit() {
+            if (RES) return;
+            const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            // hwreg(id, 0, 32): HW_ID = 4, XCC_ID = 20
+            const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+            const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+            const int idx = (int)blockIdx.x * kLdsWaves + ((int)threadIdx.x >> 6);
+            if ((threadIdx.x & 63) == 0 && idx < kStampWaves) {
+                g_lds_stamp[idx * 4 + 0] = rt0;
+                g_lds_stamp[idx * 4 + 1] = rt1;
+                g_lds_stamp[idx * 4 + 2] = t1 - t0;
+                g_lds_stamp[idx * 4 + 3] = ((unsigned long long)xcc << 32) | hw;
+            }
+        }
+    } stamp_guard{st_rt0, st_t0};
+#endif
+    if (pass_off(ctl, pass)) return;
+    if (M::SPEC && ctl->spec_stop) return;   // an earlier launch of the solve converged
+    int nst = 0;
+    if (M::REDO) {
+        nst = ctl->spec_redo;
+        if (nst <= 0) return;
+        par = ctl->spec_launch;   // re-run that launch: same source, same destination
+    }
+    lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc, nseg, wlo,
+                             whi, lds, nst, xcd_block(g));
+}
+
+// Persistent fixed-count solve: ONE launch runs nblk blocks of T sweeps
+// (par0.. launches of the per-launch form), each workgroup keeping its four
+// wave tiles for every block.  Block b of a workgroup reads the rows its
+// neighbours (the 3 x 3 workgroups around it: adjacent wave columns hold the
+// halo lanes' columns, adjacent row groups the T-row input bands) wrote in
+// block b-1, and overwrites the buffer they read in block b-1, so it starts
+// once all of them have finished block b-1 — no launch boundary, no grid-wide
+// drain, and a slow workgroup holds back only its neighbours.  Hand-off
+// (MI355X_MICROARCH.md, visibility): p' stores write through (sc1) and are
+// drained (vmcnt 0) by every wave before the workgroup's barrier, then ONE
+// lane stores the flag (agent scope); a waiting workgroup's wave 0 polls its
+// neighbours' flags (relaxed agent loads, s_sleep), and every p' load is an
+// sc1 load (never from L1); CFD_PERSIST_ACQ=1 adds an agent acquire after the
+// poll.  Flags hold epoch * 64 + blocks done; the host gives every persistent
+// launch a new epoch (never under graph capture: arguments would freeze), so
+// flags never need clearing between launches.  All
+// workgroups are resident at once (one round: lds_segments), and every spin
+// is bounded: a timeout sets persist[1] and every workgroup leaves.
+template <int T, int FAST>
+__global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_persist(
+    Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
+    Ctl *ctl, uint32_t *persist, uint32_t *host_fail, uint32_t epoch, int pass, int par0, int nblk,
+    int out_lo, int out_hi, int nwc, int nseg, int wlo, int whi, int ngrp, int acq) {
+    using M = LdsMarch<T, FAST, 4>;
+    __shared__ f2 lds[kLdsWaves * M::D * 64];
+    __shared__ int abort_s;
+    if (pass_off(ctl, pass)) return;
+    const int bid = xcd_block(g);
+    const int wc = bid % nwc, gi = bid / nwc;
+    const unsigned base = 64u * epoch;
+    uint32_t *flags = persist + kPersistFlagStride;
+    const int lane = (int)threadIdx.x & 63;
+    int nb = -1;   // wave 0, lanes 0..8: the neighbour this lane watches
+    if (lane < 9) {
+        const int c = wc + lane % 3 - 1, r = gi + lane / 3 - 1;
+        if (c >= 0 && c < nwc && r >= 0 && r < ngrp && (r != gi || c != wc)) nb = r * nwc + c;
+    }
+    for (int b = 0; b < nblk; ++b) {
+        if (b > 0) {
+            if (threadIdx.x < 64) {
+                const unsigned want = base + (unsigned)b;
+                bool fail = false;
+                for (unsigned spins = 0;; ++spins) {
+                    const unsigned v = nb >= 0 ? __hip_atomic_load(flags + (size_t)nb * kPersistFlagStride,
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                               : want;
+                    if (__all(v >= want)) break;
+                    if (spins >= (1u << 22)) {   // ~seconds: a workgroup never came
+                        fail = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (lane == 0) {
+                    abort_s = fail;
+                    if (fail) {
+                        __hip_atomic_store(persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (host_fail)   // zero-copy host word: cfd_* calls report CFD_ETIMEOUT
+                            __hip_atomic_store(host_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                }
+                if (acq) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                } else {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps loads below the poll
+                }
+            }
+            __syncthreads();
+            if (abort_s) return;   // workgroup-uniform
+        }
+        lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc, nseg, wlo,
+                              whi, lds, 0, bid);
+        // publish: every wave's write-through stores drained, then one flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(flags + (size_t)bid * kPersistFlagStride, base + (unsigned)b + 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Workgroups of k_jacobi_lds<T, FAST, RES> one CU holds at once (occupancy
@@ -628,6 +746,52 @@ void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo,
         launch_lds_t<T, 0>(g, f, pass, par, out_lo, out_hi, rs, s);
 }
 
+// The persistent form of launch_lds_t<T, 0> over nblk blocks: the same tile
+// geometry (pad, segments, weights) and one round of workgroups, all
+// resident.  false: the geometry needs more than one round (or more flags
+// than kPersistMaxGroups), nothing launched.
+template <int T>
+bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
+                          int out_hi, uint32_t epoch, hipStream_t s) {
+    const int nch = g.nx / 2;
+    const int nwc = cdiv(nch, LdsMarch<T, 1, 0>::OUTL);
+    const int nrows = out_hi - out_lo;
+    const int pad = lds_pad_bytes(g, 0);
+    const int occ = g.fastdiv == 1   ? lds_blocks_per_cu<T, 1, 0>(pad)
+                    : g.fastdiv == 2 ? lds_blocks_per_cu<T, 2, 0>(pad)
+                                     : lds_blocks_per_cu<T, 0, 0>(pad);
+    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, 0>(g, nrows, nwc, pad)
+                     : g.fastdiv == 2 ? lds_segments<T, 2, 0>(g, nrows, nwc, pad)
+                                      : lds_segments<T, 0, 0>(g, nrows, nwc, pad);
+    const int ngrp = cdiv(nseg, kLdsWaves);
+    // one round, every workgroup resident, rows for a T-row band per group
+    // residency: min(occupancy API, 6) workgroups per CU -- at 97-112 SGPRs
+    // (this kernel: 106) the hardware admits 6 where the API may say one more
+    if ((long)ngrp * nwc > (long)g.n_cu * std::min(occ, 6) || ngrp * nwc > kPersistMaxGroups ||
+        nrows < ngrp * 2 * T)
+        return false;
+    const dim3 grid(nwc * ngrp), block(kLdsWaves * 64);
+    float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
+    constexpr int kEdgeWeight = 11;
+    const int reach = T + 2;
+    const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
+    const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
+    const char *ae = getenv("CFD_PERSIST_ACQ");
+    const int acq = ae && atoi(ae) != 0;
+#define CFD_LDS_PLAUNCH(FASTV)                                                                     \
+    hipLaunchKernelGGL((k_jacobi_persist<T, FASTV>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
+                       f.persist, f.host_nonfinite ? f.host_nonfinite + 2 : nullptr, epoch, pass, par0, \
+                       nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq)
+    if (g.fastdiv == 1)
+        CFD_LDS_PLAUNCH(1);
+    else if (g.fastdiv == 2)
+        CFD_LDS_PLAUNCH(2);
+    else
+        CFD_LDS_PLAUNCH(0);
+#undef CFD_LDS_PLAUNCH
+    return true;
+}
+
 }  // namespace
 
 // per-translation-unit entry points (cfd_jacobi_lds*.hip)
@@ -635,5 +799,7 @@ void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, i
                      int out_hi, uint32_t *rs, int mode, hipStream_t s);
 void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
                    uint32_t *rs, int mode, hipStream_t s);
+bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
+                         int out_hi, uint32_t epoch, hipStream_t s);
 
 }  // namespace cfd

@@ -9,6 +9,11 @@ void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo
     launch_lds_T<8>(g, f, pass, par, out_lo, out_hi, rs, mode, s);
 }
 
+bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
+                         int out_hi, uint32_t epoch, hipStream_t s) {
+    return launch_lds_persist_t<8>(g, f, pass, par0, nblk, out_lo, out_hi, epoch, s);
+}
+
 #if CFD_LDS_STAMP
 extern "C" int cfd_diag_lds_stamps(unsigned long long *host, int nwaves) {
     if (nwaves > kStampWaves) nwaves = kStampWaves;

@@ -1525,6 +1525,12 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
         launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
 }
 
+bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,
+                           int out_lo, int out_hi, uint32_t epoch, hipStream_t s) {
+    if (out_hi <= out_lo || nblk < 1 || g.tb_kind != 5 || !f.persist) return false;
+    return launch_lds_persist8(g, f, pass, par0, nblk, out_lo, out_hi, epoch, s);
+}
+
 void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,
                         int out_lo, int out_hi, hipStream_t s) {
     if (out_hi <= out_lo) return;

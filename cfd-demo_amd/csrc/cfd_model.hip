@@ -97,6 +97,18 @@ enum FieldId { FLD_U = 0, FLD_V, FLD_PP0, FLD_PP1, FLD_RHS };
 
 }  // namespace
 
+// One per device: the last persistent Jacobi launch of this process on it
+// (k_jacobi_persist needs the whole GPU; two such launches at once could each
+// hold part of it and wait for the rest).
+struct PersistGate {
+    std::mutex mu;
+    hipEvent_t ev = nullptr;
+};
+static PersistGate &persist_gate(int device) {
+    static PersistGate gates[64];
+    return gates[device & 63];
+}
+
 struct cfd_model {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1067,7 +1079,39 @@ struct cfd_model {
                                         g.tol_enabled || it == iters - 1, stream);
                 launches = iters;
             } else {
-                for (int it = 0; it < iters;) {
+                int it = 0;
+                if (persist_env && !capturing && tmax == 8 && g.tb_kind == 5) {
+                    // the leading run of full 8-sweep blocks but the last one
+                    // (which publishes the residual) as one persistent launch
+                    int nblk = 0;
+                    for (int k = 0;;) {
+                        int T, lo, hi, exch;
+                        plan_block((int)j0, g.nyl, g.ny, 0, k, tmax, iters, &T, &lo, &hi, &exch);
+                        if (T != 8 || k + T >= iters) break;
+                        k += T;
+                        ++nblk;
+                    }
+                    if (nblk >= 2 && persist_epoch >= (1u << 25)) {
+                        // epochs wrap: clear the flags (stream-ordered) and restart
+                        HIP_TRY(hipMemsetAsync(f.persist, 0, kPersistWords * 4, stream));
+                        persist_epoch = 0;
+                    }
+                    // persistent launches of this process on one device never
+                    // overlap (each needs every workgroup resident): each waits
+                    // for the device's previous one, whichever model ran it
+                    PersistGate &gate = persist_gate(device);
+                    std::lock_guard<std::mutex> lk(gate.mu);
+                    if (nblk >= 2 && gate.ev) HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
+                    if (nblk >= 2 && launch_jacobi_persist(g, f, pass, launches, nblk, lo_g, hi_g,
+                                                           persist_epoch + 1, stream)) {
+                        if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
+                        HIP_TRY(hipEventRecord(gate.ev, stream));
+                        ++persist_epoch;
+                        it = 8 * nblk;
+                        launches = nblk;
+                    }
+                }
+                for (; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, tmax, iters, &T, &lo, &hi, &exch);
                     launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, it + T == iters,
@@ -1272,6 +1316,15 @@ struct cfd_model {
 
     bool host_driven() const { return sharded() && params.tol_enabled; }
 
+    // Persistent fixed-count solve (k_jacobi_persist); CFD_PERSIST=0 opts out.
+    // Each launch gets a new flag epoch from the host (flags start at 0).
+    bool persist_env = [] {
+        const char *e = getenv("CFD_PERSIST");
+        return !(e && atoi(e) == 0);
+    }();
+    uint32_t persist_epoch = 0;
+    bool capturing = false;   // inside update_graph's capture: no persistent launch
+
     // Speculative temporal blocking for the tolerance mode (single domain,
     // Jacobi, p' allocation within kind 5's 1 GiB buffer range); CFD_SPEC=0
     // keeps one launch per sweep with the per-sweep early exit.
@@ -1465,7 +1518,9 @@ struct cfd_model {
             const int hc0 = host_cur;
             HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
             int rc = 0;
+            capturing = true;
             for (int k = 0; k < graph_steps && !rc; ++k) rc = enqueue_update(false);
+            capturing = false;
             hipGraph_t graph = nullptr;
             const hipError_t ce = hipStreamEndCapture(stream, &graph);
             if (rc || ce != hipSuccess) {
@@ -1497,7 +1552,19 @@ struct cfd_model {
 
     int sync() {
         HIP_TRY(hipSetDevice(device));
-        return wait_done(nullptr);
+        int rc = wait_done(nullptr);
+        if (rc) return rc;
+        return persist_timeout_check();
+    }
+    // a persistent solve that gave up waiting (k_jacobi_persist) left an
+    // invalid p': report it once and solve per launch from then on
+    int persist_timeout_check() {
+        if (!h_nonfinite || !*(volatile uint32_t *)(h_nonfinite + 2)) return 0;
+        *(volatile uint32_t *)(h_nonfinite + 2) = 0u;
+        persist_env = false;
+        return fail(CFD_ETIMEOUT, "persistent Jacobi solve timed out waiting for a neighbouring "
+                                  "workgroup (not all resident); its result is invalid; "
+                                  "per-launch solves from now on");
     }
 
     int read_ctl(Ctl *out) {
@@ -1772,9 +1839,11 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         (rc = zalloc((void **)&m->slots, kSlotWords * 4)))
         return rc;
     // word 0: first non-finite step; word 1: last finished step (watchdog)
-    HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 8, hipHostMallocMapped | hipHostMallocCoherent));
+    // [0] non-finite step, [1] progress (sharded), [2] persistent-solve timeout
+    HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 16, hipHostMallocMapped | hipHostMallocCoherent));
     *(volatile uint32_t *)m->h_nonfinite = 0u;
     *(volatile uint32_t *)(m->h_nonfinite + 1) = 0u;
+    *(volatile uint32_t *)(m->h_nonfinite + 2) = 0u;
     HIP_TRY(hipHostMalloc((void **)&m->h_res, 4 * cfd_model::kResRing, hipHostMallocDefault));
     for (hipEvent_t &e : m->ev_res) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char *to = getenv("CFD_RCCL_TIMEOUT_S")) m->rccl_timeout_s = std::max(1.0, atof(to));
@@ -1866,6 +1935,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
     f.vis_slots = f.red_slots + (size_t)4 * kResSlots * kResStride;
+    f.persist = m->slots + (size_t)(kMaxSweeps + 8) * kResSlots * kResStride;
 
     Ctl c0;
     std::memset(&c0, 0, sizeof(c0));
@@ -2118,6 +2188,7 @@ int cfd_update_n(cfd_model *m, int n) {
     if (const uint32_t bad = *(volatile uint32_t *)m->h_nonfinite)
         return fail(CFD_ENONFINITE, "non-finite velocity (NaN/Inf) after step " + std::to_string(bad) +
                                         "; cfd_set_state clears it");
+    if (int rc = m->persist_timeout_check()) return rc;
     if (n <= 0) return 0;
     // solve timing: one event pair around the whole batch for the step time
     if (m->timing) {

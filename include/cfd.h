@@ -49,6 +49,10 @@ typedef enum {
                             the reference has none): cfd_update refuses to step on
                             and cfd_get_residuals reports it (filling *out all the
                             same) until cfd_set_state injects a new state */
+    CFD_ETIMEOUT = -6, /* the persistent Jacobi solve (CFD_PERSIST=1) gave up waiting for a
+                          neighbouring workgroup (they were not all resident): that
+                          solve's p' is invalid; the model falls back to one launch
+                          per block from then on */
 } cfd_status;
 
 typedef struct cfd_model cfd_model;

@@ -1,0 +1,106 @@
+"""GPU: the persistent fixed-count solve (k_jacobi_persist, CFD_PERSIST=1).
+
+One launch runs all but the last 8-sweep block of a solve; workgroups hand
+rows to their neighbours through per-workgroup flags inside the launch
+(write-through p' stores, L1-bypassing loads).  Every field must equal the
+per-launch form bit for bit -- across grids whose tiles split unevenly, with
+the obstacle masks, the second-order scheme, corrector passes, the IEEE
+division path, and a developed 4096^2 state -- and the oracle.
+"""
+import numpy as np
+import pytest
+
+from _util import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+STATE = ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
+
+
+def _states(monkeypatch, grid, params, steps, develop=0):
+    import cfdamd
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("CFD_PERSIST", env)
+        m = cfdamd.Model(grid, params, device=0)
+        try:
+            if develop:
+                m.update_n(develop)
+            m.update_n(steps)
+            out.append(m.get_state())
+        finally:
+            m.close()
+    return out
+
+
+@pytest.mark.parametrize("nx,ny,iters", [(256, 200, 50), (1024, 1024, 100), (640, 1000, 200),
+                                          (2048, 384, 40)])
+def test_persist_matches_launches_cavity(monkeypatch, nx, ny, iters):
+    import cfdamd
+    params = cfdamd.SimulationParams.cavity(400.0, iters, corrector_passes=0, tol_enabled=False)
+    a, b = _states(monkeypatch, cfdamd.cavity_grid(nx, ny), params, 12)
+    for f in STATE:
+        assert_bitwise(f"persist cavity {nx}x{ny}:{f}", b[f], a[f])
+
+
+def test_persist_matches_launches_channel_so_passes(monkeypatch):
+    """Channel with a cylinder (masks), second order, 3 corrector passes
+    (each pass's solve is persistent), non-power-of-two spacing."""
+    import cfdamd
+    grid = cfdamd.Grid(800, 264, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5))
+    params = cfdamd.SimulationParams(velocity_scheme=cfdamd.VelocityScheme.SecondOrder,
+                                     jacobi_iters=64, corrector_passes=3, tol_enabled=False)
+    a, b = _states(monkeypatch, grid, params, 10)
+    for f in STATE:
+        assert_bitwise(f"persist channel:{f}", b[f], a[f])
+
+
+@pytest.mark.timeout(300)
+def test_persist_developed_4096(monkeypatch):
+    """The bench workload from a developed state (99 % of p' non-zero)."""
+    import cfdamd
+    params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
+    a, b = _states(monkeypatch, cfdamd.cavity_grid(4096), params, 3, develop=400)
+    for f in STATE:
+        assert_bitwise(f"persist 4096:{f}", b[f], a[f])
+    assert np.count_nonzero(a["p_prime"]) > 0.9 * a["p_prime"].size
+
+
+def test_persist_matches_oracle(monkeypatch):
+    import cfdamd
+    from oracle import OracleModel
+    monkeypatch.setenv("CFD_PERSIST", "1")
+    grid = cfdamd.cavity_grid(384, 256)
+    params = cfdamd.SimulationParams.cavity(100.0, 48, corrector_passes=0, tol_enabled=False)
+    m = cfdamd.Model(grid, params, device=0)
+    o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly, bc_kind=1, viscosity=0.01, jacobi_iters=48,
+                    tol_enabled=False, corrector_passes=0)
+    try:
+        for k in range(6):
+            m.update()
+            o.update()
+        st = m.get_state()
+        for f in STATE:
+            assert_bitwise(f"persist oracle:{f}", st[f], o.field(f))
+    finally:
+        m.close()
+
+
+def test_persist_off_under_graph_replay(monkeypatch):
+    """CFD_GRAPH=1 replays captured steps with frozen kernel arguments, so
+    the captured solves run per launch (a replayed persistent launch would
+    reuse its flag epoch); the replay equals the eager persistent run."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(512, 384)
+    params = cfdamd.SimulationParams.cavity(400.0, 64, corrector_passes=0, tol_enabled=False)
+    states = []
+    for graph in ("0", "1"):
+        monkeypatch.setenv("CFD_GRAPH", graph)
+        m = cfdamd.Model(grid, params, device=0)
+        try:
+            m.update_n(13)
+            states.append(m.get_state())
+        finally:
+            m.close()
+    for f in STATE:
+        assert_bitwise(f"persist graph:{f}", states[1][f], states[0][f])

@@ -29,6 +29,9 @@ def worker(args):
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     # before the RCCL library initialises: one "host" per rank, sockets on lo
     os.environ["NCCL_HOSTID"] = f"cfd-loopback-rank{rank}"
+    # the ranks share one GPU: a persistent solve needs all its workgroups
+    # resident at once, which two processes' launches cannot both have
+    os.environ["CFD_PERSIST"] = "0"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.setdefault("NCCL_NET", "Socket")
