@@ -251,20 +251,33 @@ def time_jacobi(model, steps):
     return tm, tm["solve_ms"] / launches
 
 
+def block_kernel(model):
+    """The solve's dominant kernel as rocprofv3 names it, and the T-sweep
+    blocks one dispatch of it runs: the persistent launch (k_jacobi_persist,
+    all blocks but the last) when the model's last solve used it, else the
+    one-block launch.  PMC figures per dispatch are divided by the blocks."""
+    nb = model.persist_blocks
+    if nb > 0:
+        return f"k_jacobi_persist<8, {model.kernel_config['fastdiv']}>", nb
+    return model.jacobi_kernel["name"], 1
+
+
 def roofline_entry(model, nx, nyl, launch_ms, bench_kernel_note=None):
-    kern = model.jacobi_kernel
+    kname, nblk = block_kernel(model)
     T = model.kernel_config["temporal"]
     cells = nx * nyl
     one_pass = BYTES_PER_CELL_UPDATE * cells
     achieved = one_pass / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(kern["name"], f"{nx}x{nyl}")
+    traffic, traffic_src = pmc_traffic(kname, f"{nx}x{nyl}")
+    if traffic:
+        traffic /= nblk   # per 8-sweep block
     meas = traffic / (launch_ms * 1e-3) / 1e9 if traffic and launch_ms > 0 else None
     return {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
         "measured_hbm_GBps": meas,
         "measured_hbm_frac": meas / HBM_PEAK_GBS if meas else None,
-        "kernel": kern["name"], "slab": [nx, nyl], "sweeps_per_launch": T,
+        "kernel": kname, "blocks_per_dispatch": nblk, "slab": [nx, nyl], "sweeps_per_launch": T,
         "avg_launch_us": launch_ms * 1e3,
         "us_per_sweep": launch_ms * 1e3 / T,
         "jacobi_cell_updates_per_s": cells * T / (launch_ms * 1e-3) if launch_ms > 0 else 0.0,
@@ -274,7 +287,8 @@ def roofline_entry(model, nx, nyl, launch_ms, bench_kernel_note=None):
             "note": "12 B per cell-update x T sweeps per launch: the single-sweep figure "
                     "the launch's on-chip temporal blocking replaces"},
         "timing": "HIP events on the model stream around each step's Jacobi launch sequence "
-                  "/ launches (includes inter-launch gaps)",
+                  "/ T-sweep blocks (includes inter-launch gaps; with the persistent launch a "
+                  "'launch' is one of its blocks)",
         "note": "achieved = one-pass bytes (read p', read rhs, write p' once per launch) / "
                 "launch time; traffic = PMC bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, "
                 "gfx950 correction); FETCH_SIZE counts Infinity-Cache hits too "
@@ -286,7 +300,7 @@ def roofline_entry(model, nx, nyl, launch_ms, bench_kernel_note=None):
 VALU_ISSUE_PEAK = 1024 * 2.4e9 / 4   # wave64 VALU instructions/s: 256 CUs x 4 SIMDs, one per 4 cycles at 2.4 GHz
 
 
-def roofline_valu(kernel, slab, launch_ms):
+def roofline_valu(kernel, slab, launch_ms, blocks=1):
     """The Jacobi launch's binding resource on a MALL-resident slab is VALU
     issue: SQ_INSTS_VALU per launch from the newest committed
     PMC pass on this slab (tools/pmc_valu.py) over the measured launch time,
@@ -299,10 +313,10 @@ def roofline_valu(kernel, slab, launch_ms):
             continue
         k = d.get("kernels", {}).get(kernel)
         if k and d.get("workload") == slab and k.get("SQ_INSTS_VALU") and launch_ms > 0:
-            rate = k["SQ_INSTS_VALU"] / (launch_ms * 1e-3)
+            rate = k["SQ_INSTS_VALU"] / blocks / (launch_ms * 1e-3)
             return {"bound": "valu", "achieved": rate / 1e9, "peak": VALU_ISSUE_PEAK / 1e9,
                     "unit": "G wave64-VALU-instructions/s", "frac": rate / VALU_ISSUE_PEAK,
-                    "valu_insts_per_launch": k["SQ_INSTS_VALU"],
+                    "valu_insts_per_launch": k["SQ_INSTS_VALU"] / blocks,
                     "source": os.path.relpath(path, ROOT),
                     "note": "SQ_INSTS_VALU (PMC, same kernel and slab) / launch time; peak = 1024 "
                             "SIMDs x 1 wave64 instruction per 4 cycles x 2.4 GHz (the chip holds "
@@ -552,7 +566,8 @@ def main():
     launches = max(args.steps * model.launches_per_solve(), 1)
     launch_ms = tm["solve_ms"] / launches
     roof = roofline_entry(model, nx, model.nyl, launch_ms)
-    roof_valu = roofline_valu(kern["name"], f"{nx}x{model.nyl}", launch_ms)
+    kname, nblk = block_kernel(model)
+    roof_valu = roofline_valu(kname, f"{nx}x{model.nyl}", launch_ms, nblk)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -581,7 +596,9 @@ def main():
                 "velocity_scheme": "FirstOrder",
                 "grid": [nx, ny], "slab_per_gpu": [nx, model.nyl], "jacobi_iters": args.iters,
                 "parallelism": f"row-slab x{n}" + (f", halo depth {model.halo_depth}" if n > 1 else ""),
-                "kernel": f"{kern['name']} ({T} sweep(s)/launch, kind {kern['kind']})",
+                "kernel": (f"{kname} ({nblk} blocks of {T} sweeps in one persistent launch) + "
+                           f"{kern['name']} (the residual block)" if nblk > 1 else
+                           f"{kern['name']} ({T} sweep(s)/launch, kind {kern['kind']})"),
                 "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
                              "FMA-corrected (proven exact, 2^32 inputs)"][kcfg["fastdiv"]],
             },

@@ -401,6 +401,14 @@ class Model:
         return {"kind": kind.value, "name": name.value.decode()}
 
     @property
+    def persist_blocks(self) -> int:
+        """8-sweep blocks the last fixed-count solve ran in one persistent
+        launch (k_jacobi_persist); 0 when every block had its own launch."""
+        n = C.c_int()
+        check("cfd_get_persist_blocks", load().cfd_get_persist_blocks(self._hh(), C.byref(n)))
+        return n.value
+
+    @property
     def comm_size(self) -> int:
         """Ranks the transport reports (ncclCommCount; LocalHub size; 1)."""
         n = C.c_int()

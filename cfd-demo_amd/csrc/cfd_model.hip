@@ -1080,6 +1080,7 @@ struct cfd_model {
                 launches = iters;
             } else {
                 int it = 0;
+                last_persist_blocks = 0;
                 if (persist_env && !capturing && tmax == 8 && g.tb_kind == 5) {
                     // the leading run of full 8-sweep blocks but the last one
                     // (which publishes the residual) as one persistent launch
@@ -1107,6 +1108,7 @@ struct cfd_model {
                         if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
                         HIP_TRY(hipEventRecord(gate.ev, stream));
                         ++persist_epoch;
+                        last_persist_blocks = nblk;
                         it = 8 * nblk;
                         launches = nblk;
                     }
@@ -1323,6 +1325,7 @@ struct cfd_model {
         return !(e && atoi(e) == 0);
     }();
     uint32_t persist_epoch = 0;
+    int last_persist_blocks = 0;   // cfd_get_persist_blocks
     bool capturing = false;   // inside update_graph's capture: no persistent launch
 
     // Speculative temporal blocking for the tolerance mode (single domain,
@@ -2567,6 +2570,12 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
             snprintf(buf, sizeof buf, "k_jacobi_pipe<%d, %d, %d>", T, m->g.fastdiv, k == 3 ? 4 : 2);
         snprintf(name, name_len, "%s", buf);
     }
+    return 0;
+}
+
+int cfd_get_persist_blocks(const cfd_model *m, int *blocks) {
+    if (!m || !blocks) return fail(CFD_EINVAL, "null argument");
+    *blocks = m->last_persist_blocks;
     return 0;
 }
 

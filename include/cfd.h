@@ -222,6 +222,12 @@ int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal);
  * name_len). */
 int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len);
 
+/* Blocks of 8 sweeps the model's last fixed-count solve ran inside ONE
+ * persistent launch (k_jacobi_persist; 0: none, every block its own launch).
+ * The solve's remaining block (the one publishing the residual) is a
+ * k_jacobi_lds launch of its own. */
+int cfd_get_persist_blocks(const cfd_model *m, int *blocks);
+
 /* Host-only slab plan used by cfd_create_sharded (no device needed; the
  * multi-rank CPU tests drive the same plan):
  *   cfd_plan_slab  — global pressure rows [j0, j1) of `rank`;
