@@ -596,8 +596,9 @@ def main():
                 "velocity_scheme": "FirstOrder",
                 "grid": [nx, ny], "slab_per_gpu": [nx, model.nyl], "jacobi_iters": args.iters,
                 "parallelism": f"row-slab x{n}" + (f", halo depth {model.halo_depth}" if n > 1 else ""),
-                "kernel": (f"{kname} ({nblk} blocks of {T} sweeps in one persistent launch) + "
-                           f"{kern['name']} (the residual block)" if nblk > 1 else
+                "kernel": (f"{kname} ({nblk} blocks of {T} sweeps in one persistent launch"
+                           + (", the residual block included)" if nblk >= model.launches_per_solve()
+                              else f") + {kern['name']} launches for the rest") if nblk > 1 else
                            f"{kern['name']} ({T} sweep(s)/launch, kind {kern['kind']})"),
                 "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
                              "FMA-corrected (proven exact, 2^32 inputs)"][kcfg["fastdiv"]],

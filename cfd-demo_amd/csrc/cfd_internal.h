@@ -171,10 +171,11 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
                          int out_lo, int out_hi, int res, hipStream_t s);
 // nblk consecutive 8-sweep kind-5 blocks (no residual) in ONE persistent
 // launch whose workgroups hand rows to their neighbours through flags
-// (k_jacobi_persist); returns false (nothing launched) where the one-round
-// geometry does not apply
+// (k_jacobi_persist); res_it >= 0: the last block is the solve's last and
+// publishes sweep res_it's residual; returns false (nothing launched) where
+// the one-round geometry does not apply
 bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,
-                           int out_lo, int out_hi, uint32_t epoch, hipStream_t s);
+                           int out_lo, int out_hi, uint32_t epoch, int res_it, hipStream_t s);
 // The block kernels behind it: k_jacobi_tb (T <= 4, cfd_jacobi_tb1.hip) and
 // the prefetch-pipelined march with 4 or 2 columns per lane (T <= 8,
 // cfd_jacobi_pipe4.hip / cfd_jacobi_pipe2.hip).
@@ -188,7 +189,7 @@ void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int p
 // kind 5: the same march with its rhs window in LDS (cfd_jacobi_lds.hip, T <= 8);
 // mode 2 / 3: the speculative launch / its re-run (launch_jacobi_spec)
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
-                         int out_hi, uint32_t epoch, hipStream_t s);
+                         int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s);
 void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
                 int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0);
 // Speculative temporal blocking for the tolerance mode (model.rs:748-819):

@@ -107,11 +107,12 @@ constexpr int ring_depth(int T, int PD, int G) {
 // run-time stage count Ctl::spec_redo < T (stores only the segment's rows).
 template <int T, int FAST, int MODE>
 struct LdsMarch {
-    static constexpr bool RES = MODE == 1, SPEC = MODE == 2, REDO = MODE == 3;
+    static constexpr bool RES = MODE == 1 || MODE == 5, SPEC = MODE == 2, REDO = MODE == 3;
     // MODE 4 (PERSIST): a block of k_jacobi_persist; p' moves between
     // workgroups inside the launch, so its loads bypass L1 and its stores
-    // write through (sc1 both ways, MI355X_MICROARCH.md visibility rules)
-    static constexpr bool PERSIST = MODE == 4;
+    // write through (sc1 both ways, MI355X_MICROARCH.md visibility rules).
+    // MODE 5: its last block, which also publishes the residual (RES)
+    static constexpr bool PERSIST = MODE == 4 || MODE == 5;
     static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
     static constexpr int PST_AUX = PERSIST ? 16 : CFD_LDS_ST_AUX;
     // Stage s of slot v computes row k - s - off(s).  With G = 1 (off = 0)
@@ -571,8 +572,9 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 template <int T, int FAST>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_persist(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
-    Ctl *ctl, uint32_t *persist, uint32_t *host_fail, uint32_t epoch, int pass, int par0, int nblk,
-    int out_lo, int out_hi, int nwc, int nseg, int wlo, int whi, int ngrp, int acq) {
+    Ctl *ctl, uint32_t *persist, uint32_t *host_fail, uint32_t *res_slots, uint32_t epoch, int pass,
+    int par0, int nblk, int out_lo, int out_hi, int nwc, int nseg, int wlo, int whi, int ngrp,
+    int acq) {
     using M = LdsMarch<T, FAST, 4>;
     __shared__ f2 lds[kLdsWaves * M::D * 64];
     __shared__ int abort_s;
@@ -620,6 +622,11 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
             }
             __syncthreads();
             if (abort_s) return;   // workgroup-uniform
+        }
+        if (res_slots && b == nblk - 1) {   // the solve's last block: its residual too
+            lds_block<T, FAST, 5>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi, nwc, nseg,
+                                  wlo, whi, lds, 0, bid);
+            return;
         }
         lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc, nseg, wlo,
                               whi, lds, 0, bid);
@@ -752,7 +759,7 @@ void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo,
 // than kPersistMaxGroups), nothing launched.
 template <int T>
 bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
-                          int out_hi, uint32_t epoch, hipStream_t s) {
+                          int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s) {
     const int nch = g.nx / 2;
     const int nwc = cdiv(nch, LdsMarch<T, 1, 0>::OUTL);
     const int nrows = out_hi - out_lo;
@@ -780,8 +787,8 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
     const int acq = ae && atoi(ae) != 0;
 #define CFD_LDS_PLAUNCH(FASTV)                                                                     \
     hipLaunchKernelGGL((k_jacobi_persist<T, FASTV>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
-                       f.persist, f.host_nonfinite ? f.host_nonfinite + 2 : nullptr, epoch, pass, par0, \
-                       nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq)
+                       f.persist, f.host_nonfinite ? f.host_nonfinite + 2 : nullptr, rs, epoch, pass, \
+                       par0, nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq)
     if (g.fastdiv == 1)
         CFD_LDS_PLAUNCH(1);
     else if (g.fastdiv == 2)
@@ -800,6 +807,6 @@ void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, i
 void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
                    uint32_t *rs, int mode, hipStream_t s);
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
-                         int out_hi, uint32_t epoch, hipStream_t s);
+                         int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s);
 
 }  // namespace cfd

@@ -10,8 +10,8 @@ void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo
 }
 
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
-                         int out_hi, uint32_t epoch, hipStream_t s) {
-    return launch_lds_persist_t<8>(g, f, pass, par0, nblk, out_lo, out_hi, epoch, s);
+                         int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s) {
+    return launch_lds_persist_t<8>(g, f, pass, par0, nblk, out_lo, out_hi, epoch, rs, s);
 }
 
 #if CFD_LDS_STAMP

@@ -1526,9 +1526,10 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
 }
 
 bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,
-                           int out_lo, int out_hi, uint32_t epoch, hipStream_t s) {
+                           int out_lo, int out_hi, uint32_t epoch, int res_it, hipStream_t s) {
     if (out_hi <= out_lo || nblk < 1 || g.tb_kind != 5 || !f.persist) return false;
-    return launch_lds_persist8(g, f, pass, par0, nblk, out_lo, out_hi, epoch, s);
+    uint32_t *rs = res_it >= 0 ? f.err_slots + (size_t)res_it * kResSlots * kResStride : nullptr;
+    return launch_lds_persist8(g, f, pass, par0, nblk, out_lo, out_hi, epoch, rs, s);
 }
 
 void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,

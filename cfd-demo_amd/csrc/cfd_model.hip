@@ -1082,13 +1082,18 @@ struct cfd_model {
                 int it = 0;
                 last_persist_blocks = 0;
                 if (persist_env && !capturing && tmax == 8 && g.tb_kind == 5) {
-                    // the leading run of full 8-sweep blocks but the last one
-                    // (which publishes the residual) as one persistent launch
-                    int nblk = 0;
-                    for (int k = 0;;) {
+                    // the leading run of full 8-sweep blocks as one persistent
+                    // launch, the solve's last block (which publishes the
+                    // residual) included when it is a full block too
+                    int nblk = 0, res_it = -1;
+                    for (int k = 0; k < iters;) {
                         int T, lo, hi, exch;
                         plan_block((int)j0, g.nyl, g.ny, 0, k, tmax, iters, &T, &lo, &hi, &exch);
-                        if (T != 8 || k + T >= iters) break;
+                        if (T != 8) break;
+                        if (k + T >= iters) {
+                            if (persist_res_env) res_it = iters - 1;
+                            else break;
+                        }
                         k += T;
                         ++nblk;
                     }
@@ -1104,7 +1109,7 @@ struct cfd_model {
                     std::lock_guard<std::mutex> lk(gate.mu);
                     if (nblk >= 2 && gate.ev) HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
                     if (nblk >= 2 && launch_jacobi_persist(g, f, pass, launches, nblk, lo_g, hi_g,
-                                                           persist_epoch + 1, stream)) {
+                                                           persist_epoch + 1, res_it, stream)) {
                         if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
                         HIP_TRY(hipEventRecord(gate.ev, stream));
                         ++persist_epoch;
@@ -1322,6 +1327,12 @@ struct cfd_model {
     // Each launch gets a new flag epoch from the host (flags start at 0).
     bool persist_env = [] {
         const char *e = getenv("CFD_PERSIST");
+        return !(e && atoi(e) == 0);
+    }();
+    // the solve's last (residual) block inside the persistent launch too;
+    // CFD_PERSIST_RES=0 launches it on its own
+    bool persist_res_env = [] {
+        const char *e = getenv("CFD_PERSIST_RES");
         return !(e && atoi(e) == 0);
     }();
     uint32_t persist_epoch = 0;

@@ -224,8 +224,8 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
 
 /* Blocks of 8 sweeps the model's last fixed-count solve ran inside ONE
  * persistent launch (k_jacobi_persist; 0: none, every block its own launch).
- * The solve's remaining block (the one publishing the residual) is a
- * k_jacobi_lds launch of its own. */
+ * Blocks after them (shorter ones of an uneven split) are k_jacobi_lds
+ * launches of their own. */
 int cfd_get_persist_blocks(const cfd_model *m, int *blocks);
 
 /* Host-only slab plan used by cfd_create_sharded (no device needed; the
