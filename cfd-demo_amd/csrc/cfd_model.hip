@@ -1043,6 +1043,31 @@ struct cfd_model {
         return 0;
     }
 
+    // nblk >= 2 eight-sweep blocks on rows [lo, hi) in one persistent launch
+    // (k_jacobi_persist); *done = false when it does not apply.  Persistent
+    // launches of this process on one device never overlap (each needs every
+    // workgroup resident): each waits for the device's previous one, whichever
+    // model ran it.
+    int launch_persist(int pass, int par0, int nblk, int lo, int hi, int res_it, bool *done) {
+        *done = false;
+        if (nblk < 2 || !persist_env || capturing || g.tb_kind != 5) return 0;
+        if (persist_epoch >= (1u << 25)) {
+            // epochs wrap: clear the flags (stream-ordered) and restart
+            HIP_TRY(hipMemsetAsync(f.persist, 0, kPersistWords * 4, stream));
+            persist_epoch = 0;
+        }
+        PersistGate &gate = persist_gate(device);
+        std::lock_guard<std::mutex> lk(gate.mu);
+        if (gate.ev) HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
+        if (!launch_jacobi_persist(g, f, pass, par0, nblk, lo, hi, persist_epoch + 1, res_it, stream))
+            return 0;
+        if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(gate.ev, stream));
+        ++persist_epoch;
+        *done = true;
+        return 0;
+    }
+
     int enqueue_solve(int pass) {
         if (params.pressure_solver == CFD_SOLVER_SOR) return enqueue_sor(pass);
         if (params.pressure_solver == CFD_SOLVER_MULTIGRID) return enqueue_mg(pass);
@@ -1097,22 +1122,10 @@ struct cfd_model {
                         k += T;
                         ++nblk;
                     }
-                    if (nblk >= 2 && persist_epoch >= (1u << 25)) {
-                        // epochs wrap: clear the flags (stream-ordered) and restart
-                        HIP_TRY(hipMemsetAsync(f.persist, 0, kPersistWords * 4, stream));
-                        persist_epoch = 0;
-                    }
-                    // persistent launches of this process on one device never
-                    // overlap (each needs every workgroup resident): each waits
-                    // for the device's previous one, whichever model ran it
-                    PersistGate &gate = persist_gate(device);
-                    std::lock_guard<std::mutex> lk(gate.mu);
-                    if (nblk >= 2 && gate.ev) HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
-                    if (nblk >= 2 && launch_jacobi_persist(g, f, pass, launches, nblk, lo_g, hi_g,
-                                                           persist_epoch + 1, res_it, stream)) {
-                        if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
-                        HIP_TRY(hipEventRecord(gate.ev, stream));
-                        ++persist_epoch;
+                    bool done = false;
+                    int rc = launch_persist(pass, launches, nblk, lo_g, hi_g, res_it, &done);
+                    if (rc) return rc;
+                    if (done) {
                         last_persist_blocks = nblk;
                         it = 8 * nblk;
                         launches = nblk;
@@ -1134,6 +1147,7 @@ struct cfd_model {
             // launch's interior rows, whose T sweeps read no rhs ghost row
             // (the march for output rows [a, b) loads rhs rows [a-T, b+T)),
             // run on stream; the edge rows follow once the ghosts are in.
+            last_persist_blocks = 0;
             const bool rhs_ovl = overlap && tmax > 1 && !pp_ghosts_shallow && iters > 0;
             bool rhs_pending = false;
             // whatever path leaves this block, stream waits for the rhs exchange
@@ -1203,6 +1217,31 @@ struct cfd_model {
                 } else if (tmax == 1) {
                     launch_jacobi_sweep(g, f, pass, it, lo, hi, res, stream);
                 } else {
+                    // a run of 8-sweep blocks between two exchanges as one
+                    // persistent launch over the first block's rows: later
+                    // blocks recompute ghost rows past their valid band too,
+                    // which only feed ghost rows and are replaced by the next
+                    // exchange (owned rows stay inside every block's band)
+                    int nrun = 0;
+                    if (T == 8 && tmax == 8 && !exch && !res && persist_sharded_env)
+                        for (int k = it; k < iters;) {
+                            int T2, lo2, hi2, ex2;
+                            plan_block(g.j0, g.nyl, g.ny, g.hg, k, tmax, iters, &T2, &lo2, &hi2, &ex2);
+                            if (T2 != 8 || ex2 || k + T2 == iters) break;
+                            k += T2;
+                            ++nrun;
+                        }
+                    bool done = false;
+                    if (nrun >= 2) {
+                        int rc = launch_persist(pass, launches, nrun, lo, hi, -1, &done);
+                        if (rc) return rc;
+                    }
+                    if (done) {
+                        it += 8 * nrun;
+                        launches += nrun;
+                        last_persist_blocks += nrun;
+                        continue;
+                    }
                     launch_jacobi_block(g, f, pass, it, launches, T, lo, hi, res, stream);
                 }
                 it += T;
@@ -1333,6 +1372,12 @@ struct cfd_model {
     // CFD_PERSIST_RES=0 launches it on its own
     bool persist_res_env = [] {
         const char *e = getenv("CFD_PERSIST_RES");
+        return !(e && atoi(e) == 0);
+    }();
+    // slabs: the blocks between two p' exchanges as one persistent launch
+    // (CFD_PERSIST_SHARDED=0: per launch)
+    bool persist_sharded_env = [] {
+        const char *e = getenv("CFD_PERSIST_SHARDED");
         return !(e && atoi(e) == 0);
     }();
     uint32_t persist_epoch = 0;

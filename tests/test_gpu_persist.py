@@ -104,3 +104,54 @@ def test_persist_off_under_graph_replay(monkeypatch):
             m.close()
     for f in STATE:
         assert_bitwise(f"persist graph:{f}", states[1][f], states[0][f])
+
+
+def _run_slabs(monkeypatch, n, grid, params, steps, depth, sharded_env):
+    import threading
+    import cfdamd
+    monkeypatch.setenv("CFD_HALO_DEPTH", str(depth))
+    monkeypatch.setenv("CFD_PERSIST_SHARDED", sharded_env)
+    hub = cfdamd.LocalHub(n)
+    out, models, errors = [None] * n, [None] * n, []
+
+    def worker(r):
+        try:
+            m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=r, local_hub=hub)
+            models[r] = m
+            m.update_n(steps)
+            m.synchronize()
+            out[r] = (m.get_state(), m.persist_blocks)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    for m in models:
+        if m is not None:
+            m.close()
+    hub.close()
+    if errors:
+        raise errors[0]
+    return out
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [2, 4])
+def test_persist_runs_between_exchanges_on_slabs(monkeypatch, n):
+    """Slabs with 32 ghost rows: the 8-sweep blocks between two p' exchanges
+    run as one persistent launch over the first block's band (later blocks
+    recompute ghost rows past their valid band, which the exchange replaces);
+    owned rows equal the per-launch slabs bit for bit."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(512, 1024 * n // 2)
+    params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
+    a = _run_slabs(monkeypatch, n, grid, params, 6, 32, "0")
+    b = _run_slabs(monkeypatch, n, grid, params, 6, 32, "1")
+    assert all(pb == 0 for _, pb in a), [pb for _, pb in a]
+    assert all(pb >= 2 for _, pb in b), [pb for _, pb in b]
+    for r in range(n):
+        for f in STATE:
+            assert_bitwise(f"slab {r}/{n}:{f}", b[r][0][f], a[r][0][f])
