@@ -103,6 +103,7 @@ enum FieldId { FLD_U = 0, FLD_V, FLD_PP0, FLD_PP1, FLD_RHS };
 struct PersistGate {
     std::mutex mu;
     hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;   // the stream of the device's last persistent launch
 };
 static PersistGate &persist_gate(int device) {
     static PersistGate gates[64];
@@ -1058,11 +1059,21 @@ struct cfd_model {
         }
         PersistGate &gate = persist_gate(device);
         std::lock_guard<std::mutex> lk(gate.mu);
-        if (gate.ev) HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
+        // a stream orders its own launches; after another model's stream ran
+        // the device's last persistent launch, this one waits for everything
+        // that stream has enqueued so far (a single model records nothing)
+        if (gate.last && gate.last != stream) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            (void)hipStreamIsCapturing(gate.last, &cs);
+            if (cs == hipStreamCaptureStatusNone) {
+                if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(gate.ev, gate.last));
+                HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
+            }
+        }
         if (!launch_jacobi_persist(g, f, pass, par0, nblk, lo, hi, persist_epoch + 1, res_it, stream))
             return 0;
-        if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(gate.ev, stream));
+        gate.last = stream;
         ++persist_epoch;
         *done = true;
         return 0;
@@ -1634,6 +1645,11 @@ struct cfd_model {
     }
 
     void destroy() {
+        {   // the persistent-launch gate must not keep this model's stream
+            PersistGate &gate = persist_gate(device);
+            std::lock_guard<std::mutex> lk(gate.mu);
+            if (gate.last == stream) gate.last = nullptr;
+        }
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm) ncclCommDestroy(comm);
