@@ -38,6 +38,10 @@ constexpr int kResStride = 16;
 // persistent-solve words (k_jacobi_persist): [1] timeout flag, then one
 // hand-off flag per workgroup on a 64-B line of its own
 constexpr int kPersistFlagStride = 16;
+// flag = epoch << kPersistBlockBits | blocks done: room for every block of the
+// longest solve (kMaxSweeps / 8 = 512), epochs below 2^(32 - bits)
+constexpr int kPersistBlockBits = 10;
+static_assert((1 << kPersistBlockBits) > kMaxSweeps / 8, "persistent flag layout");
 constexpr int kPersistMaxGroups = 4096;
 constexpr size_t kPersistWords = (size_t)(kPersistMaxGroups + 1) * kPersistFlagStride;
 constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 8) * kResSlots * kResStride + kPersistWords;

@@ -564,7 +564,8 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 // lane stores the flag (agent scope); a waiting workgroup's wave 0 polls its
 // neighbours' flags (relaxed agent loads, s_sleep), and every p' load is an
 // sc1 load (never from L1); CFD_PERSIST_ACQ=1 adds an agent acquire after the
-// poll.  Flags hold epoch * 64 + blocks done; the host gives every persistent
+// poll.  Flags hold epoch * 2^kPersistBlockBits + blocks done (a solve has at
+// most kMaxSweeps / 8 = 512 blocks); the host gives every persistent
 // launch a new epoch (never under graph capture: arguments would freeze), so
 // flags never need clearing between launches.  All
 // workgroups are resident at once (one round: lds_segments), and every spin
@@ -581,7 +582,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
     if (pass_off(ctl, pass)) return;
     const int bid = xcd_block(g);
     const int wc = bid % nwc, gi = bid / nwc;
-    const unsigned base = 64u * epoch;
+    const unsigned base = epoch << kPersistBlockBits;
     uint32_t *flags = persist + kPersistFlagStride;
     const int lane = (int)threadIdx.x & 63;
     int nb = -1;   // wave 0, lanes 0..8: the neighbour this lane watches

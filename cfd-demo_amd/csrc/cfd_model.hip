@@ -1052,7 +1052,7 @@ struct cfd_model {
     int launch_persist(int pass, int par0, int nblk, int lo, int hi, int res_it, bool *done) {
         *done = false;
         if (nblk < 2 || !persist_env || capturing || g.tb_kind != 5) return 0;
-        if (persist_epoch >= (1u << 25)) {
+        if (persist_epoch + 1 >= (1u << (32 - kPersistBlockBits))) {
             // epochs wrap: clear the flags (stream-ordered) and restart
             HIP_TRY(hipMemsetAsync(f.persist, 0, kPersistWords * 4, stream));
             persist_epoch = 0;

@@ -33,7 +33,7 @@ def _states(monkeypatch, grid, params, steps, develop=0):
     return out
 
 
-@pytest.mark.parametrize("nx,ny,iters", [(256, 200, 50), (1024, 1024, 100), (640, 1000, 200),
+@pytest.mark.parametrize("nx,ny,iters", [(256, 200, 50), (1024, 1024, 100), (640, 1000, 200), (1024, 1024, 1200),
                                           (2048, 384, 40)])
 def test_persist_matches_launches_cavity(monkeypatch, nx, ny, iters):
     import cfdamd
