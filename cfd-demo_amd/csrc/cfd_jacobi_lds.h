@@ -147,6 +147,7 @@ struct LdsMarch {
     f2 *ring;
     int lane;
     int k_first, S, lo_clamp, hi_clamp, nch, g_first, g_last, g_top, g_zero, row_bytes;
+    int wbase;   // first row of the wave's buffer window (descriptors start there)
     int ch, vo_ld, vo_st, abase, dir;
     bool e0, e1;         // residual columns (kCol slots)
     // the Jacobi divisors and their reciprocals (uniform values, not a pointer
@@ -171,12 +172,12 @@ struct LdsMarch {
         vrow = vrow < k_first + S ? vrow : k_first + S - 1;
         int row = act(vrow);
         row = row < lo_clamp ? lo_clamp : (row > hi_clamp ? hi_clamp : row);
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo_ld, (row - lo_clamp) * row_bytes, AUX);
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo_ld, (row - wbase) * row_bytes, AUX);
         return (f2){__uint_as_float(v.x), __uint_as_float(v.y)};
     }
     __device__ __forceinline__ void st(const f2 &x, int row) const {
         const u32x2 v = {__float_as_uint(x.x), __float_as_uint(x.y)};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - lo_clamp) * row_bytes, PST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - wbase) * row_bytes, PST_AUX);
     }
 
     // One reference update (model.rs:775-793) of the lane's column pair.
@@ -428,10 +429,18 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     const int si = (ctl->cur + par) & 1;
     float *src_alloc = si ? pb : pa;
     float *dst_alloc = si ? pa : pb;
-    const int pbytes = (g.nyl + 2 * g.hg) * nx * 4;
-    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc, 0, pbytes, 0x00020000);
-    w.rs_d = __builtin_amdgcn_make_buffer_rsrc(dst_alloc, 0, pbytes, 0x00020000);
-    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)g.hg * nx), 0, pbytes,
+    // buffer descriptors over the rows this wave can touch, [r0 - T, r1 + T)
+    // clamped to the allocation, with a row of margin: offsets stay small at
+    // any field size, so a parked lane's voffset (kFar) plus the row offset
+    // never wraps 2^32 and always lands past the window (fields of any size,
+    // not just up to 1 GiB)
+    const int wb = max(w.lo_clamp, r0 - T - 1), wt = min(w.hi_clamp, r1 + T);
+    w.wbase = wb;
+    const long woff = (long)(wb - w.lo_clamp) * nx;
+    const int wbytes = (wt - wb + 1) * nx * 4;
+    w.rs_p = __builtin_amdgcn_make_buffer_rsrc(src_alloc + woff, 0, wbytes, 0x00020000);
+    w.rs_d = __builtin_amdgcn_make_buffer_rsrc(dst_alloc + woff, 0, wbytes, 0x00020000);
+    w.rs_r = __builtin_amdgcn_make_buffer_rsrc((void *)(rhs - (long)g.hg * nx + woff), 0, wbytes,
                                                0x00020000);
     w.dx_sq = g.dx_sq;
     w.r_dx_sq = g.r_dx_sq;

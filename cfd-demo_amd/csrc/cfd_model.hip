@@ -1396,7 +1396,7 @@ struct cfd_model {
     bool capturing = false;   // inside update_graph's capture: no persistent launch
 
     // Speculative temporal blocking for the tolerance mode (single domain,
-    // Jacobi, p' allocation within kind 5's 1 GiB buffer range); CFD_SPEC=0
+    // Jacobi, kind-5 kernels at any field size); CFD_SPEC=0
     // keeps one launch per sweep with the per-sweep early exit.
     bool spec_env = [] {
         const char *e = getenv("CFD_SPEC");
@@ -1404,8 +1404,7 @@ struct cfd_model {
     }();
     bool spec_mode() const {
         return spec_env && !sharded() && g.tol_enabled &&
-               params.pressure_solver == CFD_SOLVER_JACOBI &&
-               (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)g.nx * 4u <= (1ull << 30);
+               params.pressure_solver == CFD_SOLVER_JACOBI;
     }
 
     // u* <- u, v* <- v and the divergence at the head of a corrector pass
@@ -1855,9 +1854,11 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         const int k = atoi(kv);
         g.tb_kind = (k == 3 || k == 4 || k == 5) ? k : 1;
     }
-    // the pipelined kernels park masked lanes at a far voffset that must not
-    // wrap past 2^32 when the row offset is added: slabs up to 1 GiB per field
-    if ((uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u > (1ull << 30)) g.tb_kind = 1;
+    // the pipelined kernels (kinds 3/4) park masked lanes at a far voffset
+    // that must not wrap past 2^32 when the row offset is added: slabs up to
+    // 1 GiB per field (kind 5 bases its descriptors at each wave's rows)
+    if (g.tb_kind != 5 && (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)nx * 4u > (1ull << 30))
+        g.tb_kind = 1;
     m->t_max = g.tb_kind == 3 ? 6 : 4;
     {
         // kind 4 past the 256 MB Infinity Cache: 8 sweeps per launch halve the

@@ -155,3 +155,29 @@ def test_persist_runs_between_exchanges_on_slabs(monkeypatch, n):
     for r in range(n):
         for f in STATE:
             assert_bitwise(f"slab {r}/{n}:{f}", b[r][0][f], a[r][0][f])
+
+
+@pytest.mark.timeout(300)
+def test_kind5_fields_over_1GiB(monkeypatch):
+    """A single-domain grid whose p' field exceeds 1 GiB (16384 x 17408,
+    1.14 GiB per field): kind 5 -- per-wave buffer windows, so a parked
+    lane's offset never wraps -- runs it (persistently) and equals kind 1
+    (CFD_TB_KIND=1, the former fallback) bit for bit."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(16384, 17408)
+    params = cfdamd.SimulationParams.cavity(1000.0, 16, corrector_passes=0, tol_enabled=False)
+    states = []
+    for kind in ("1", "5"):
+        monkeypatch.setenv("CFD_TB_KIND", kind)
+        m = cfdamd.Model(grid, params, device=0)
+        try:
+            assert m.jacobi_kernel["kind"] == int(kind), m.jacobi_kernel
+            m.update_n(8)   # past the inlet ramp's first steps: p' non-zero under the lid
+            st = m.get_state()
+            states.append({f: st[f] for f in ("u", "v", "p_prime", "rhs")})
+            del st
+        finally:
+            m.close()
+    for f in ("u", "v", "p_prime", "rhs"):
+        assert_bitwise(f"kind5 >1GiB:{f}", states[1][f], states[0][f])
+    assert np.count_nonzero(states[1]["p_prime"]) > 0
