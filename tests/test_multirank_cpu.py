@@ -305,3 +305,22 @@ def test_plan_slab_partition_properties():
             assert all(rows[k][1] == rows[k + 1][0] for k in range(n - 1))
             sizes = [b - a for a, b in rows]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_single_domain_blocks_split_evenly():
+    """Unsharded solves (hg = 0): ceil(iters / t_max) launches -- as many as
+    t_max-sized blocks -- whose sweep counts differ by at most one and run
+    longest first (50 = 8 + 6 x 7, never a short tail launch); the whole
+    interior rows every time.  The persistent solve takes the leading run
+    of 8-sweep blocks from this split."""
+    for t_max in range(1, 9):
+        for iters in range(1, 260):
+            it, Ts = 0, []
+            while it < iters:
+                T, lo, hi, ex = plan_block(0, 96, 96, 0, it, t_max, iters)
+                assert 1 <= T <= t_max and (lo, hi, ex) == (1, 95, False)
+                Ts.append(T)
+                it += T
+            assert it == iters
+            assert len(Ts) == -(-iters // t_max), (t_max, iters, Ts)
+            assert max(Ts) - min(Ts) <= 1 and Ts == sorted(Ts, reverse=True), (t_max, iters, Ts)
