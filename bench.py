@@ -114,13 +114,27 @@ def cpu_baseline(nx, ny, iters, re, budget_s, state, threads=1, max_steps=5):
                         f"{1e3 * max(times):.0f}); host {model}, {ncpu} cpus"}
 
 
-def oracle_from_state(nx, ny, iters, re, state, threads, scheme=0, passes=0, tol=0):
+def oracle_from_state(nx, ny, iters, re, state, threads, scheme=0, passes=0, tol=0, grid=None,
+                      params=None):
+    """The oracle at `state`: the nx x ny cavity (Re, iters, scheme, passes,
+    tol), or `grid` / `params` (cfdamd Grid / SimulationParams) when given."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from oracle import OracleModel
     orc.set_threads(threads)
-    m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
-                    jacobi_iters=iters, corrector_passes=passes, tol_enabled=tol, scheme=scheme)
+    if grid is not None:
+        c = grid.obstacle
+        p = params
+        m = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly,
+                        cylinder=(c.center_x, c.center_y, c.radius) if c else None,
+                        dt=p.dt, viscosity=p.viscosity, target_inlet_velocity=p.target_inlet_velocity,
+                        scheme=int(p.velocity_scheme), inlet_profile=int(p.inlet_profile),
+                        jacobi_iters=p.jacobi_iters, corrector_passes=p.corrector_passes,
+                        tol_enabled=int(p.tol_enabled), p_tol=p.p_tol, bc_kind=int(p.bc_kind),
+                        pressure_solver=int(p.pressure_solver))
+    else:
+        m = OracleModel(nx, ny, float(nx) / float(ny), 1.0, bc_kind=1, viscosity=1.0 / re,
+                        jacobi_iters=iters, corrector_passes=passes, tol_enabled=tol, scheme=scheme)
     for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs"):
         m.field(k)[:] = state[k]
     sc = m.scalars()
@@ -149,6 +163,72 @@ def parity_developed_step(model, nx, ny, iters, re, state, threads, **mode):
     if int(g["jacobi_sweeps_total"]) != int(s.jacobi_sweeps_total):
         bad.append("jacobi_sweeps_total")
     return not bad, bad
+
+
+def reference_default_leg(args, cfdamd, device, develop=200, steps=20, cpu_steps=3):
+    """The reference's own design point: default_grid() -- the 800 x 264
+    channel with the cylinder, lx 30, ly 10 (src/app.rs:33-53) -- under the
+    default SimulationParams (model.rs:44-55: dt 0.005, nu 1e-6, <= 50 sweeps
+    per solve with the 1e-4 early exit, <= 20 corrector passes,
+    model.rs:696-724, 748-819), FirstOrder and SecondOrder.  Developed from
+    rest for `develop` untimed steps, then `steps` timed; the kernel names the
+    solve runs (its spacings are not powers of two: the IEEE or FMA-corrected
+    division forms), one step bitwise against the oracle from the developed
+    state, and the oracle's 1-thread ms/step on the same state beside it."""
+    out = {"workload": "default_grid() 800x264 channel, cylinder r 0.75 at (7.5, 5), lx 30, ly 10 "
+                       "(app.rs:33-53); SimulationParams::default() (model.rs:44-55): <=50 "
+                       "sweeps/solve, early exit 1e-4, <=20 corrector passes",
+           "developed": f"{develop} steps from rest"}
+    for scheme in (cfdamd.VelocityScheme.FirstOrder, cfdamd.VelocityScheme.SecondOrder):
+        grid = cfdamd.default_grid()
+        params = cfdamd.SimulationParams(velocity_scheme=scheme)
+        m = cfdamd.Model(grid, params, device=device)
+        m.update_n(develop)
+        m.synchronize()
+        s0 = m.get_residuals().jacobi_sweeps_total
+        t0 = time.perf_counter()
+        m.update_n(steps)
+        m.synchronize()
+        el = time.perf_counter() - t0
+        sweeps = m.get_residuals().jacobi_sweeps_total - s0
+        kc = m.kernel_config
+        e = {"steps": steps, "ms_per_step": 1e3 * el / steps, "sweeps_per_step": sweeps / steps,
+             "cell_updates_per_s": grid.nx * grid.ny * sweeps / el,
+             "kernel": m.jacobi_kernel["name"],
+             "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
+                          "FMA-corrected (proven exact, 2^32 inputs)"][kc["fastdiv"]]}
+        state = m.get_state()
+        if not args.no_parity:
+            o, orc = oracle_from_state(0, 0, 0, 0, state, cpu_threads(), grid=grid, params=params)
+            m.update()
+            o.update()
+            orc.set_threads(1)
+            g = m.get_state()
+            import numpy as np
+            bad = [k for k in ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
+                   if not np.array_equal(g[k].view(np.uint32), o.field(k).view(np.uint32))]
+            sc = o.scalars()
+            if int(g["jacobi_sweeps_total"]) != int(sc.jacobi_sweeps_total):
+                bad.append("jacobi_sweeps_total")
+            for k, want in (("dt", sc.dt), ("last_p_residual", sc.p), ("simulation_time", sc.time)):
+                if np.float32(g[k]).view(np.uint32) != np.float32(want).view(np.uint32):
+                    bad.append(k)
+            e["parity_developed_step"] = not bad
+            if bad:
+                e["parity_differ"] = bad
+        m.close()
+        if not args.no_cpu_baseline:
+            o, orc = oracle_from_state(0, 0, 0, 0, state, 1, grid=grid, params=params)
+            ts = []
+            for _ in range(cpu_steps):
+                t0 = time.perf_counter()
+                o.update()
+                ts.append(time.perf_counter() - t0)
+            med = sorted(ts)[len(ts) // 2]
+            e["cpu_oracle_1thread_ms_per_step"] = 1e3 * med
+            e["gpu_over_cpu"] = med / (el / steps)
+        out[scheme.name] = e
+    return out
 
 
 def phase_window(model, steps):
@@ -238,6 +318,62 @@ def parity_mode_leg(args, cfdamd, device, n, re, fixed_iters, steps=5):
             out["parity_differ"] = bad
     m.close()
     return out
+
+
+STATE_KEYS = ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
+SCALAR_KEYS = ("dt", "simulation_time", "simulation_step", "last_p_residual", "last_u_residual",
+               "last_v_residual", "jacobi_sweeps_total")
+
+
+def parity_sharded_step(model, dist, rank, world, grid, params, device):
+    """N > 1: one more step on the slabs, checked against the same step of a
+    single-domain GPU model of the whole grid started from the gathered slab
+    state (rank 0; 16384 x 8192 fits one MI355X).  The single domain is
+    itself bitwise against the oracle (parity_developed_step at N = 1, the
+    test suite), so a True here carries the oracle's parity to the N-GPU run
+    that was just timed: every word of u, v, p, u*, v*, p', rhs and every
+    scalar of every rank.  Collective: every rank calls it."""
+    import numpy as np
+    import cfdamd
+    pre = model.get_state()
+    model.update()
+    post = model.get_state()
+    mine = (model.j0, model.j1, {k: pre[k] for k in STATE_KEYS}, {k: post[k] for k in STATE_KEYS},
+            {k: pre[k] for k in SCALAR_KEYS}, {k: post[k] for k in SCALAR_KEYS})
+    del pre, post
+    objs = [None] * world if rank == 0 else None
+    dist.gather_object(mine, objs, dst=0)
+    del mine
+    if rank != 0:
+        return None
+    t0 = time.perf_counter()
+    try:
+        g_pre = cfdamd.assemble_slabs([(o[0], o[1], o[2]) for o in objs], grid.nx)
+        g_post = cfdamd.assemble_slabs([(o[0], o[1], o[3]) for o in objs], grid.nx)
+    except ValueError as e:   # a shared v face row differs between two slabs
+        return {"ok": False, "differ": [str(e)]}
+    sc_pre, sc_post = objs[0][4], [o[5] for o in objs]
+    del objs
+    ref = cfdamd.Model(grid, params, device=device)
+    try:
+        ref.set_state(**g_pre, **sc_pre)
+        del g_pre
+        ref.update()
+        r = ref.get_state()
+    finally:
+        ref.close()
+    bad = [k for k in STATE_KEYS if not np.array_equal(r[k].view(np.uint32), g_post[k].view(np.uint32))]
+
+    def same(a, b):
+        return (np.float32(a).view(np.uint32) == np.float32(b).view(np.uint32)
+                if isinstance(a, (float, np.floating)) else int(a) == int(b))
+    for rk, sp in enumerate(sc_post):
+        bad += [f"{k} (rank {rk})" for k in SCALAR_KEYS if not same(sp[k], r[k])]
+    return {"ok": not bad, "differ": bad,
+            "detail": f"1 step from step {int(sc_pre['simulation_step'])} on the {world} slabs vs "
+                      f"a single-domain {grid.nx}x{grid.ny} model on device {device} from the "
+                      f"gathered slab state: every word of u, v, p, u*, v*, p', rhs and the "
+                      f"scalars of every rank compared ({time.perf_counter() - t0:.1f} s)"}
 
 
 def time_jacobi(model, steps):
@@ -451,6 +587,8 @@ def main():
                     help="skip the second-order upwind leg at N=1")
     ap.add_argument("--no-parity-mode", action="store_true",
                     help="skip the reference-control-flow legs (C2, C3) at N=1")
+    ap.add_argument("--no-reference-default", action="store_true",
+                    help="skip the reference's default_grid() channel leg at N=1")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="seconds the self-launched ranks of --gpus N may take")
     ap.add_argument("--dry-run", action="store_true",
@@ -468,7 +606,8 @@ def main():
         # trick): every rank on device 0, each its own RCCL "host" so RCCL
         # connects them through its socket transport; set before RCCL loads
         os.environ["NCCL_HOSTID"] = f"cfd-bench-rank{rank}"
-        os.environ["CFD_PERSIST"] = "0"   # ranks share the GPU (persistent solves need it whole)
+        # persistent solves stay on: the ticketed launch completes with the
+        # ranks' kernels sharing the GPU (the exact SCALE configuration)
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
         os.environ.setdefault("NCCL_NET", "Socket")
@@ -568,6 +707,24 @@ def main():
     roof = roofline_entry(model, nx, model.nyl, launch_ms)
     kname, nblk = block_kernel(model)
     roof_valu = roofline_valu(kname, f"{nx}x{model.nyl}", launch_ms, nblk)
+    geometry = model.jacobi_geometry(persist=nblk > 1)
+    multi = {}
+    if n > 1:
+        # collective legs, after the timed steps (every rank takes part):
+        # per-rank phase and RCCL exchange times, then the sharded parity step
+        ph = phase_window(model, 5)
+        ex = model.timing_exchange_ms()
+        mine = {"rank": rank, "predict_march_us": ph["predict_march_us"],
+                "correct_finish_us": ph["correct_finish_us"], "solve_us": ph["solve_us"],
+                "step_us_events": ph["step_us_events"],
+                "exchange_us_per_step": 1e3 * ex["exchange_ms"] / ph["steps"],
+                "exchanges_per_step": ex["exchanges"] / ph["steps"], "geometry": geometry}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        multi["rank_phases"] = gathered
+        if not args.no_parity:
+            multi["parity_sharded_step"] = parity_sharded_step(model, dist, rank, world, grid,
+                                                               params, local)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -605,6 +762,7 @@ def main():
             },
             "roofline": roof,
             "roofline_valu": roof_valu,
+            "jacobi_geometry": geometry,
             "solve_fraction_of_step": tm["solve_ms"] / tm["step_ms"] if tm["step_ms"] else None,
             # a timed-mode step moves 2,498 B per pressure cell
             # when every pass streams its fields (P = 1 solve, K = 200 sweeps);
@@ -619,6 +777,13 @@ def main():
             "final_step": int(state["simulation_step"]), "final_dt": float(state["dt"]),
             "fields_finite": finite and res is not None,
         }
+        if n > 1:
+            out["rank_phases"] = multi["rank_phases"]
+            ps = multi.get("parity_sharded_step")
+            if ps is not None:
+                out["parity_sharded_step"] = ps["ok"]
+                out["parity_sharded_step_detail"] = ps.get("detail", "") + (
+                    "" if ps["ok"] else f"; differ: {ps['differ']}")
         if n == 1 and not args.no_parity and out["fields_finite"]:
             ok, bad = parity_developed_step(model, nx, ny, args.iters, args.re, state,
                                             cpu_threads())
@@ -637,6 +802,8 @@ def main():
                 "C3": parity_mode_leg(args, cfdamd, local, 4096, 1000.0, 200)}
         if n == 1 and not args.no_control:
             out["roofline_control"] = control_run(args, cfdamd, local)
+        if n == 1 and not args.no_reference_default:
+            out["reference_default"] = reference_default_leg(args, cfdamd, local)
         if n == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(nx, ny, args.iters, args.re, args.cpu_budget, state)
             nt = cpu_threads()

@@ -99,6 +99,29 @@ def default_grid() -> Grid:
     return Grid(800, 264, lx, ly, Cylinder(lx / 4.0, ly / 2.0, 0.75))
 
 
+def assemble_slabs(slabs, nx: int) -> dict:
+    """Global flat fields from the states of the row slabs of one grid:
+    `slabs` = [(j0, j1, state)] in rank order (state as Model.get_state()
+    returns it).  Owned rows are concatenated; v and v* take the shared face
+    row j1 of each slab from the slab above (both compute it, bit-identically:
+    raises ValueError when they differ)."""
+    out = {}
+    for f in ("u", "p", "p_prime", "u_star", "rhs"):
+        out[f] = np.concatenate([s[f] for (_, _, s) in slabs])
+    for f in ("v", "v_star"):
+        parts = []
+        for k, (j0, j1, s) in enumerate(slabs):
+            rows = s[f].reshape(j1 - j0 + 1, nx)
+            last = k == len(slabs) - 1
+            parts.append(rows if last else rows[:-1])
+            if not last:
+                nxt = slabs[k + 1][2][f].reshape(-1, nx)[0]
+                if not np.array_equal(rows[-1].view(np.uint32), nxt.view(np.uint32)):
+                    raise ValueError(f"{f}: shared face row {j1} differs between slabs {k} and {k + 1}")
+        out[f] = np.concatenate(parts).ravel()
+    return out
+
+
 def cavity_grid(nx: int, ny: Optional[int] = None) -> Grid:
     """Build-defined lid-driven cavity: unit height, dx = dy."""
     ny = nx if ny is None else ny
@@ -352,6 +375,14 @@ class Model:
               load().cfd_timing_phase_ms(self._hh(), C.byref(a), C.byref(b)))
         return {"predict_ms": a.value, "finish_ms": b.value}
 
+    def timing_exchange_ms(self) -> dict:
+        """RCCL exchange groups + all-reduces of the last timing window with
+        phases on (sharded models over RCCL; 0 otherwise)."""
+        a, n = C.c_double(), C.c_uint64()
+        check("cfd_timing_exchange_ms",
+              load().cfd_timing_exchange_ms(self._hh(), C.byref(a), C.byref(n)))
+        return {"exchange_ms": a.value, "exchanges": int(n.value)}
+
     @property
     def kernel_config(self) -> dict:
         fd, tb = C.c_int(), C.c_int()
@@ -399,6 +430,15 @@ class Model:
         check("cfd_get_jacobi_kernel",
               load().cfd_get_jacobi_kernel(self._hh(), C.byref(kind), name, 96))
         return {"kind": kind.value, "name": name.value.decode()}
+
+    def jacobi_geometry(self, persist: bool = True) -> dict:
+        """Tile geometry of the 8-sweep kind-5 launch (cfd_get_jacobi_geometry):
+        LDS pad bytes, workgroups per CU of the round, wave columns, segments."""
+        v = [C.c_int32() for _ in range(4)]
+        check("cfd_get_jacobi_geometry",
+              load().cfd_get_jacobi_geometry(self._hh(), int(bool(persist)), *(C.byref(x) for x in v)))
+        return dict(lds_pad=v[0].value, wgs_per_cu=v[1].value, wave_cols=v[2].value,
+                    segments=v[3].value)
 
     @property
     def persist_blocks(self) -> int:

@@ -35,15 +35,17 @@ constexpr int kMaxPasses = 64;     // corrector passes + 1
 // the 4 step maxima own red_slots likewise.  Slots are zero between uses.
 constexpr int kResSlots = 32;
 constexpr int kResStride = 16;
-// persistent-solve words (k_jacobi_persist): [1] timeout flag, then one
-// hand-off flag per workgroup on a 64-B line of its own
+// persistent-solve words (k_jacobi_persist), one 64-B line each: line 0 [1]
+// the abort flag; lines 1 and 2 the task tickets of even / odd epochs; then
+// one hand-off flag per tile
 constexpr int kPersistFlagStride = 16;
+constexpr int kPersistHeadLines = 3;
 // flag = epoch << kPersistBlockBits | blocks done: room for every block of the
 // longest solve (kMaxSweeps / 8 = 512), epochs below 2^(32 - bits)
 constexpr int kPersistBlockBits = 10;
 static_assert((1 << kPersistBlockBits) > kMaxSweeps / 8, "persistent flag layout");
-constexpr int kPersistMaxGroups = 4096;
-constexpr size_t kPersistWords = (size_t)(kPersistMaxGroups + 1) * kPersistFlagStride;
+constexpr int kPersistMaxGroups = 16384;   // tiles (wave columns x row groups)
+constexpr size_t kPersistWords = (size_t)(kPersistMaxGroups + kPersistHeadLines) * kPersistFlagStride;
 constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 8) * kResSlots * kResStride + kPersistWords;
 
 // Device-resident control block: every data-dependent decision of
@@ -180,6 +182,12 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
 // the one-round geometry does not apply
 bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,
                            int out_lo, int out_hi, uint32_t epoch, int res_it, hipStream_t s);
+// The tile geometry of the T = 8 kind-5 launch over rows [out_lo, out_hi)
+// (persist: the persistent form's): dynamic LDS pad, workgroups per CU the
+// round is sized for, wave columns, wave segments per column
+// (cfd_jacobi_lds8.hip).
+void lds_geometry8(const Geom &g, int out_lo, int out_hi, bool persist, int *pad, int *occ, int *nwc,
+                   int *nseg);
 // The block kernels behind it: k_jacobi_tb (T <= 4, cfd_jacobi_tb1.hip) and
 // the prefetch-pipelined march with 4 or 2 columns per lane (T <= 8,
 // cfd_jacobi_pipe4.hip / cfd_jacobi_pipe2.hip).

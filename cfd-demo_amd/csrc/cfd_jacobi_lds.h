@@ -561,55 +561,92 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 }
 
 // Persistent fixed-count solve: ONE launch runs nblk blocks of T sweeps
-// (par0.. launches of the per-launch form), each workgroup keeping its four
-// wave tiles for every block.  Block b of a workgroup reads the rows its
-// neighbours (the 3 x 3 workgroups around it: adjacent wave columns hold the
-// halo lanes' columns, adjacent row groups the T-row input bands) wrote in
-// block b-1, and overwrites the buffer they read in block b-1, so it starts
-// once all of them have finished block b-1 — no launch boundary, no grid-wide
-// drain, and a slow workgroup holds back only its neighbours.  Hand-off
-// (MI355X_MICROARCH.md, visibility): p' stores write through (sc1) and are
-// drained (vmcnt 0) by every wave before the workgroup's barrier, then ONE
-// lane stores the flag (agent scope); a waiting workgroup's wave 0 polls its
-// neighbours' flags (relaxed agent loads, s_sleep), and every p' load is an
-// sc1 load (never from L1); CFD_PERSIST_ACQ=1 adds an agent acquire after the
-// poll.  Flags hold epoch * 2^kPersistBlockBits + blocks done (a solve has at
-// most kMaxSweeps / 8 = 512 blocks); the host gives every persistent
-// launch a new epoch (never under graph capture: arguments would freeze), so
-// flags never need clearing between launches.  All
-// workgroups are resident at once (one round: lds_segments), and every spin
-// is bounded: a timeout sets persist[1] and every workgroup leaves.
+// (par0.. launches of the per-launch form) over ntiles tiles (tile = the four
+// wave segments of one workgroup of the per-launch form).  The work is
+// nblk * ntiles tasks (block b, tile t), numbered block-major; workgroups take
+// task tickets IN ORDER from one counter (a returning atomic, fetched one task
+// ahead) until the tickets run out.  Task (b, t) reads the rows that tile t
+// and its 3 x 3 neighbours (adjacent wave columns hold the halo lanes'
+// columns, adjacent row groups the T-row input bands) wrote in block b-1, and
+// overwrites the buffer they read in block b-1, so it starts once all nine
+// have finished block b-1 — no launch boundary, no grid-wide drain, and a slow
+// task holds back only its neighbours.
+//
+// Why tickets: every task a waiting workgroup depends on has a smaller
+// ticket, so it was taken by a workgroup that is running, and (by induction)
+// it finishes.  The launch therefore completes whatever number of its
+// workgroups the GPU holds at once — a co-tenant kernel, another model's
+// stream, RCCL kernels or a grid larger than one round only slow it down.
+// (The r3 form bound tile w to workgroup w and needed all of them resident:
+// a co-tenant could strand it until its spin limit, with p' left invalid.)
+//
+// Hand-off (MI355X_MICROARCH.md "Valid forms", Consumer, always): p' stores
+// write through (sc1) and every wave drains them (s_waitcnt vmcnt(0)) before
+// the workgroup's barrier, then ONE lane stores the tile's flag (agent scope);
+// a waiting workgroup's wave 0 polls the nine flags (relaxed agent loads,
+// s_sleep), then ONE agent acquire (buffer_inv sc1) + vmcnt(0) + the
+// workgroup barrier before any p' load.  The launch runs several workgroups
+// per CU, outside the table under which sc1 loads alone may replace the
+// acquire, so the acquire stays (acq = 1, CFD_PERSIST_ACQ=0 opts out for
+// measurement only).  Flags hold epoch * 2^kPersistBlockBits + blocks done (a
+// solve has at most kMaxSweeps / 8 = 512 blocks); the host gives every
+// persistent launch a new epoch (never under graph capture: arguments would
+// freeze), so flags never need clearing between launches; launch e zeroes
+// the ticket counter of launch e+1 (the two alternate by epoch parity).
+// Waits are bounded by wall time (s_memrealtime, `deadline` ticks of 10 ns):
+// past it the waiter sets the abort word persist[1], every workgroup leaves
+// at its next poll or at entry, and a zero-copy host word makes the model's
+// next cfd_* call report CFD_ETIMEOUT (a fault, not a residency effect).
 template <int T, int FAST>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_persist(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *persist, uint32_t *host_fail, uint32_t *res_slots, uint32_t epoch, int pass,
     int par0, int nblk, int out_lo, int out_hi, int nwc, int nseg, int wlo, int whi, int ngrp,
-    int acq) {
+    int acq, uint32_t deadline) {
     using M = LdsMarch<T, FAST, 4>;
     __shared__ f2 lds[kLdsWaves * M::D * 64];
-    __shared__ int abort_s;
+    // task_s[i & 1]: the ticket of the workgroup's task i (double-buffered: a
+    // wave may still read entry i after the barrier while entry i+1 is written)
+    __shared__ int task_s[2], abort_s;
+    uint32_t *tickets = persist + (1 + (epoch & 1)) * kPersistFlagStride;
+    if (blockIdx.x == 0 && threadIdx.x == 0)   // the next launch's counter (stream-ordered)
+        __hip_atomic_store(persist + (1 + ((epoch + 1) & 1)) * kPersistFlagStride, 0u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (pass_off(ctl, pass)) return;
-    const int bid = xcd_block(g);
-    const int wc = bid % nwc, gi = bid / nwc;
     const unsigned base = epoch << kPersistBlockBits;
-    uint32_t *flags = persist + kPersistFlagStride;
+    uint32_t *flags = persist + kPersistHeadLines * kPersistFlagStride;
+    const int ntiles = ngrp * nwc, ntask = nblk * ntiles;
     const int lane = (int)threadIdx.x & 63;
-    int nb = -1;   // wave 0, lanes 0..8: the neighbour this lane watches
-    if (lane < 9) {
-        const int c = wc + lane % 3 - 1, r = gi + lane / 3 - 1;
-        if (c >= 0 && c < nwc && r >= 0 && r < ngrp && (r != gi || c != wc)) nb = r * nwc + c;
+    constexpr int kTicketThread = (kLdsWaves - 1) * 64;   // the last wave fetches tickets (wave 0 polls)
+    if (threadIdx.x == 0) {
+        // fail fast after an abort (every later launch of the model too)
+        const bool dead = __hip_atomic_load(persist + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        task_s[0] = dead ? ntask : (int)__hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
     }
-    for (int b = 0; b < nblk; ++b) {
+    __syncthreads();
+    int t = task_s[0];
+    for (int i = 1; t < ntask; ++i) {
+        const int b = t / ntiles, tile = t - b * ntiles;
         if (b > 0) {
             if (threadIdx.x < 64) {
+                // lanes 0..8 watch the tile and its neighbours, lane 9 the abort word
+                const int wc = tile % nwc, gi = tile / nwc;
+                const int c = wc + lane % 3 - 1, r = gi + lane / 3 - 1;
+                const uint32_t *w = lane < 9 ? (c >= 0 && c < nwc && r >= 0 && r < ngrp
+                                                    ? flags + (size_t)(r * nwc + c) * kPersistFlagStride
+                                                    : nullptr)
+                                             : (lane == 9 ? persist + 1 : nullptr);
                 const unsigned want = base + (unsigned)b;
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 bool fail = false;
-                for (unsigned spins = 0;; ++spins) {
-                    const unsigned v = nb >= 0 ? __hip_atomic_load(flags + (size_t)nb * kPersistFlagStride,
-                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                               : want;
-                    if (__all(v >= want)) break;
-                    if (spins >= (1u << 22)) {   // ~seconds: a workgroup never came
+                for (;;) {
+                    const unsigned v = w ? __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : 0u;
+                    const bool ok = lane < 9 ? (w == nullptr || v >= want) : v == 0u;
+                    if (__all(ok)) break;
+                    if (__any(lane == 9 && v != 0u) ||
+                        __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)deadline) {
                         fail = true;
                         break;
                     }
@@ -633,19 +670,25 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
             __syncthreads();
             if (abort_s) return;   // workgroup-uniform
         }
-        if (res_slots && b == nblk - 1) {   // the solve's last block: its residual too
+        // the next ticket, one task ahead: its latency overlaps this task's
+        // first loads (on the ticket wave, not on the polling wave)
+        uint32_t next = 0;
+        if (threadIdx.x == kTicketThread)
+            next = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (res_slots && b == nblk - 1)   // the solve's last block: its residual too
             lds_block<T, FAST, 5>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi, nwc, nseg,
-                                  wlo, whi, lds, 0, bid);
-            return;
-        }
-        lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc, nseg, wlo,
-                              whi, lds, 0, bid);
+                                  wlo, whi, lds, 0, tile);
+        else
+            lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc, nseg,
+                                  wlo, whi, lds, 0, tile);
         // publish: every wave's write-through stores drained, then one flag
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == kTicketThread) task_s[i & 1] = (int)next;
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(flags + (size_t)bid * kPersistFlagStride, base + (unsigned)b + 1u,
+            __hip_atomic_store(flags + (size_t)tile * kPersistFlagStride, base + (unsigned)b + 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = task_s[i & 1];
     }
 }
 
@@ -662,6 +705,11 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
 // HBM-streaming slabs, where more waves in flight pay (8192^2: 23.8 vs 24.5
 // us/sweep padded), nor on the speculative launches (ab_pad_parity.log).
 // CFD_LDS_PAD=<bytes> forces one value on every launch.
+// The test is on the OWNED rows (r4): every slab of the weak-scaling series
+// (4096^2, 8192x2048 and 16384x1024, 16.78 M cells, 201 MB) runs the same
+// geometry; with the hg ghost rows counted, the 16384x1024 slab (32 ghost rows
+// each side, 214 MB) fell past the threshold and ran unpadded while the
+// others were padded.  The ghost rows (6 % at C5) still fit the 256 MiB cache.
 inline int lds_pad_bytes(const Geom &g, int mode) {
     static const int forced = [] {
         const char *e = getenv("CFD_LDS_PAD");
@@ -669,7 +717,7 @@ inline int lds_pad_bytes(const Geom &g, int mode) {
     }();
     if (forced >= 0) return forced;
     constexpr uint64_t kMallResident = 200ull << 20;
-    const uint64_t ws = 3ull * (uint64_t)(g.nyl + 2 * g.hg) * (uint64_t)g.nx * 4u;
+    const uint64_t ws = 3ull * (uint64_t)g.nyl * (uint64_t)g.nx * 4u;
     return mode <= 1 && ws <= kMallResident ? 24 * 1024 : 0;
 }
 template <int T, int FAST, int MODE>
@@ -693,8 +741,10 @@ int lds_blocks_per_cu(int pad) {
 // SIMD gets its waves at once and the same march length, so no CU waits for a
 // second, partial round — or whole multiples of a round when a round would
 // make segments longer than kMaxRows.
+// occ_override > 0: size the round for that many workgroups per CU (the
+// persistent kernel's own occupancy)
 template <int T, int FAST, int MODE>
-int lds_segments(const Geom &g, int nrows, int nwc, int pad) {
+int lds_segments(const Geom &g, int nrows, int nwc, int pad, int occ_override = 0) {
     if (g.tb_rows > 0) return cdiv(nrows, g.tb_rows);
     constexpr int kMaxRows = 160, kMinRows = 8;
     // CFD_LDS_BPC caps the workgroups per CU a round is sized for (below the
@@ -703,7 +753,7 @@ int lds_segments(const Geom &g, int nrows, int nwc, int pad) {
         const char *e = getenv("CFD_LDS_BPC");
         return e ? std::max(1, atoi(e)) : 0;
     }();
-    const int occ = lds_blocks_per_cu<T, FAST, MODE>(pad);
+    const int occ = occ_override > 0 ? occ_override : lds_blocks_per_cu<T, FAST, MODE>(pad);
     const int bpc = bpc_cap > 0 ? std::min(occ, bpc_cap) : occ;
     const int wgs_per_col = std::max(1, g.n_cu * bpc / nwc);
     const int per_round = kLdsWaves * wgs_per_col;
@@ -763,10 +813,33 @@ void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo,
         launch_lds_t<T, 0>(g, f, pass, par, out_lo, out_hi, rs, s);
 }
 
+// Workgroups of k_jacobi_persist<T, FAST> one CU holds at once with `pad`
+// bytes of dynamic LDS: the occupancy API on the launched kernel itself,
+// capped by the SGPR rule of MI355X_MICROARCH.md (Residency): at 97-112 SGPRs
+// the hardware admits 6 four-wave workgroups where the API may say 7.  Used to
+// size the tiles so one round of workgroups covers them; residency is no
+// longer a correctness condition (tickets, k_jacobi_persist).
+template <int T, int FAST>
+int persist_blocks_per_cu(int pad) {
+    static int cache[2] = {0, 0};
+    int &nb = cache[pad > 0 ? 1 : 0];
+    if (nb == 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &n, reinterpret_cast<const void *>(&k_jacobi_persist<T, FAST>), kLdsWaves * 64, pad) !=
+                hipSuccess ||
+            n < 1)
+            n = 1;
+        nb = std::min(n, 6);
+    }
+    return nb;
+}
+
 // The persistent form of launch_lds_t<T, 0> over nblk blocks: the same tile
-// geometry (pad, segments, weights) and one round of workgroups, all
-// resident.  false: the geometry needs more than one round (or more flags
-// than kPersistMaxGroups), nothing launched.
+// geometry (pad, segments, weights), its round sized by the persistent
+// kernel's own occupancy; a grid of min(tiles, one round) workgroups takes
+// the tasks by ticket.  false (nothing launched): more tiles than
+// kPersistMaxGroups flags, or row groups shorter than two T-row bands.
 template <int T>
 bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
                           int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s) {
@@ -774,31 +847,42 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
     const int nwc = cdiv(nch, LdsMarch<T, 1, 0>::OUTL);
     const int nrows = out_hi - out_lo;
     const int pad = lds_pad_bytes(g, 0);
-    const int occ = g.fastdiv == 1   ? lds_blocks_per_cu<T, 1, 0>(pad)
-                    : g.fastdiv == 2 ? lds_blocks_per_cu<T, 2, 0>(pad)
-                                     : lds_blocks_per_cu<T, 0, 0>(pad);
-    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, 0>(g, nrows, nwc, pad)
-                     : g.fastdiv == 2 ? lds_segments<T, 2, 0>(g, nrows, nwc, pad)
-                                      : lds_segments<T, 0, 0>(g, nrows, nwc, pad);
+    const int occ = g.fastdiv == 1   ? persist_blocks_per_cu<T, 1>(pad)
+                    : g.fastdiv == 2 ? persist_blocks_per_cu<T, 2>(pad)
+                                     : persist_blocks_per_cu<T, 0>(pad);
+    const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, 0>(g, nrows, nwc, pad, occ)
+                     : g.fastdiv == 2 ? lds_segments<T, 2, 0>(g, nrows, nwc, pad, occ)
+                                      : lds_segments<T, 0, 0>(g, nrows, nwc, pad, occ);
     const int ngrp = cdiv(nseg, kLdsWaves);
-    // one round, every workgroup resident, rows for a T-row band per group
-    // residency: min(occupancy API, 6) workgroups per CU -- at 97-112 SGPRs
-    // (this kernel: 106) the hardware admits 6 where the API may say one more
-    if ((long)ngrp * nwc > (long)g.n_cu * std::min(occ, 6) || ngrp * nwc > kPersistMaxGroups ||
-        nrows < ngrp * 2 * T)
-        return false;
-    const dim3 grid(nwc * ngrp), block(kLdsWaves * 64);
+    // rows for a T-row band per group: a task's input rows lie in its 3 x 3
+    // neighbourhood
+    if (ngrp * nwc > kPersistMaxGroups || nrows < ngrp * 2 * T) return false;
+    // CFD_PERSIST_GRID=<n>: launch n workgroups (tests: fewer than the tiles,
+    // or more than the GPU holds at once); default one round
+    // (read per launch, like the two knobs below: one getenv per solve)
+    const char *ge = getenv("CFD_PERSIST_GRID");
+    const int grid_env = ge ? std::max(1, atoi(ge)) : 0;
+    const long round = (long)g.n_cu * occ;
+    const int nwg = grid_env > 0 ? grid_env : (int)std::min<long>((long)ngrp * nwc, round);
+    const dim3 grid(nwg), block(kLdsWaves * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     constexpr int kEdgeWeight = 11;
     const int reach = T + 2;
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
+    // the agent acquire after each poll (CFD_PERSIST_ACQ=0: measurement only)
     const char *ae = getenv("CFD_PERSIST_ACQ");
-    const int acq = ae && atoi(ae) != 0;
+    const int acq = ae ? (atoi(ae) != 0) : 1;
+    // wait deadline in s_memrealtime ticks (100 MHz): CFD_PERSIST_DEADLINE_US,
+    // default 10 s (a wait that long is a fault; time-sliced GPUs stay far
+    // below it)
+    const char *de = getenv("CFD_PERSIST_DEADLINE_US");
+    const double dl_us = de ? std::max(0.0, atof(de)) : 10e6;
+    const uint32_t deadline = (uint32_t)std::min(4.0e9, dl_us * 100.0);
 #define CFD_LDS_PLAUNCH(FASTV)                                                                     \
     hipLaunchKernelGGL((k_jacobi_persist<T, FASTV>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
                        f.persist, f.host_nonfinite ? f.host_nonfinite + 2 : nullptr, rs, epoch, pass, \
-                       par0, nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq)
+                       par0, nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq, deadline)
     if (g.fastdiv == 1)
         CFD_LDS_PLAUNCH(1);
     else if (g.fastdiv == 2)

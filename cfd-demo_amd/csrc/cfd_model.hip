@@ -97,9 +97,10 @@ enum FieldId { FLD_U = 0, FLD_V, FLD_PP0, FLD_PP1, FLD_RHS };
 
 }  // namespace
 
-// One per device: the last persistent Jacobi launch of this process on it
-// (k_jacobi_persist needs the whole GPU; two such launches at once could each
-// hold part of it and wait for the rest).
+// One per device: the last persistent Jacobi launch of this process on it.
+// Opt-in serialization (CFD_PERSIST_GATE=1): the r3 launch needed the whole
+// GPU, two at once could each hold part of it and wait for the rest; the
+// ticketed r4 launch (k_jacobi_persist) runs beside anything.
 struct PersistGate {
     std::mutex mu;
     hipEvent_t ev = nullptr;
@@ -162,15 +163,18 @@ struct cfd_model {
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> solve_events;
-    // per-phase events (cfd_timing_phases): predictors + first divergence,
-    // and the corrector / finish, summed at cfd_timing_end
+    // per-phase events (cfd_timing_phases): [0] predictors + first
+    // divergence, [1] the corrector / finish, [2] the RCCL halo exchanges and
+    // all-reduces (each on the stream it runs on, waiting for the peer
+    // included), summed at cfd_timing_end
     bool timing_phases = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> phase_events[2];
-    double phase_ms[2] = {0.0, 0.0};
-    hipEvent_t phase_mark(int ph, bool end) {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> phase_events[3];
+    double phase_ms[3] = {0.0, 0.0, 0.0};
+    uint64_t phase_count[3] = {0, 0, 0};
+    hipEvent_t phase_mark(int ph, bool end, hipStream_t st = nullptr) {
         if (!(timing && timing_phases)) return nullptr;
         hipEvent_t e = take_event();
-        (void)hipEventRecord(e, stream);
+        (void)hipEventRecord(e, st ? st : stream);
         if (end) phase_events[ph].back().second = e;
         else phase_events[ph].emplace_back(e, nullptr);
         return e;
@@ -217,9 +221,11 @@ struct cfd_model {
         if (!st) st = stream;
         if (hub) return exchange_local(id, kind, depth, st);
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        phase_mark(2, false, st);
         RCCL_TRY(ncclGroupStart());
         int rc = exchange_ops(id, kind, depth, st);
         RCCL_OP(ncclGroupEnd());
+        phase_mark(2, true, st);
         return rc;
     }
 
@@ -279,10 +285,12 @@ struct cfd_model {
             return exchange_local(FLD_V, HALO_V, 2, st);
         }
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        phase_mark(2, false, st);
         RCCL_TRY(ncclGroupStart());
         int rc = exchange_ops(FLD_U, HALO_U, 2, st);
         if (!rc) rc = exchange_ops(FLD_V, HALO_V, 2, st);
         RCCL_OP(ncclGroupEnd());
+        phase_mark(2, true, st);
         return rc;
     }
 
@@ -308,7 +316,9 @@ struct cfd_model {
             return 0;
         }
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        phase_mark(2, false);
         RCCL_OP(ncclAllReduce(dev, dev, n, ncclUint32, ncclMax, comm, stream));
+        phase_mark(2, true);
         return 0;
     }
 
@@ -1059,10 +1069,13 @@ struct cfd_model {
         }
         PersistGate &gate = persist_gate(device);
         std::lock_guard<std::mutex> lk(gate.mu);
-        // a stream orders its own launches; after another model's stream ran
-        // the device's last persistent launch, this one waits for everything
-        // that stream has enqueued so far (a single model records nothing)
-        if (gate.last && gate.last != stream) {
+        // a stream orders its own launches; with CFD_PERSIST_GATE=1, after
+        // another model's stream ran the device's last persistent launch, this
+        // one waits for everything that stream has enqueued so far.  Off by
+        // default since r4: the ticketed launch completes beside any other
+        // kernel (k_jacobi_persist), so the gate is no longer needed for
+        // correctness
+        if (persist_gate_env && gate.last && gate.last != stream) {
             hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
             (void)hipStreamIsCapturing(gate.last, &cs);
             if (cs == hipStreamCaptureStatusNone) {
@@ -1390,6 +1403,12 @@ struct cfd_model {
     bool persist_sharded_env = [] {
         const char *e = getenv("CFD_PERSIST_SHARDED");
         return !(e && atoi(e) == 0);
+    }();
+    // serialize persistent launches of different models on one device
+    // (CFD_PERSIST_GATE=1; see launch_persist)
+    bool persist_gate_env = [] {
+        const char *e = getenv("CFD_PERSIST_GATE");
+        return e && atoi(e) != 0;
     }();
     uint32_t persist_epoch = 0;
     int last_persist_blocks = 0;   // cfd_get_persist_blocks
@@ -2557,8 +2576,7 @@ int cfd_timing_begin(cfd_model *m) {
     m->ev_next = 0;
     m->solve_events.clear();
     m->step_events.clear();
-    m->phase_events[0].clear();
-    m->phase_events[1].clear();
+    for (auto &pe : m->phase_events) pe.clear();
     m->timed_sweeps = 0;
     m->timed_launches = 0;
     m->timed_steps = 0;
@@ -2580,13 +2598,15 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
         HIP_TRY(hipEventElapsedTime(&ms, m->step_events[k], m->step_events[k + 1]));
         t_ms += ms;
     }
-    for (int ph = 0; ph < 2; ++ph) {
+    for (int ph = 0; ph < 3; ++ph) {
         m->phase_ms[ph] = 0.0;
+        m->phase_count[ph] = 0;
         for (auto &pr : m->phase_events[ph]) {
             float ms = 0.f;
             if (!pr.second) continue;
             HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
             m->phase_ms[ph] += ms;
+            ++m->phase_count[ph];
         }
         m->phase_events[ph].clear();
     }
@@ -2611,6 +2631,13 @@ int cfd_timing_phase_ms(const cfd_model *m, double *predict_ms, double *finish_m
     if (!m) return fail(CFD_EINVAL, "null model");
     if (predict_ms) *predict_ms = m->phase_ms[0];
     if (finish_ms) *finish_ms = m->phase_ms[1];
+    return 0;
+}
+
+int cfd_timing_exchange_ms(const cfd_model *m, double *exchange_ms, uint64_t *exchanges) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (exchange_ms) *exchange_ms = m->phase_ms[2];
+    if (exchanges) *exchanges = m->phase_count[2];
     return 0;
 }
 
@@ -2643,6 +2670,25 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
             snprintf(buf, sizeof buf, "k_jacobi_pipe<%d, %d, %d>", T, m->g.fastdiv, k == 3 ? 4 : 2);
         snprintf(name, name_len, "%s", buf);
     }
+    return 0;
+}
+
+int cfd_get_jacobi_geometry(const cfd_model *m, int persist, int *lds_pad, int *wgs_per_cu,
+                            int *wave_cols, int *segments) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    if (hipSetDevice(m->device) != hipSuccess) return fail(CFD_EHIP, "hipSetDevice");
+    // the rows of the solve's first 8-sweep block (a slab's owned rows plus
+    // the ghost rows that block recomputes)
+    int T, lo, hi, exch;
+    plan_block((int)m->j0, m->g.nyl, m->g.ny, m->sharded() ? m->g.hg : 0, 0, 8,
+               std::max(8, m->params.jacobi_iters), &T, &lo, &hi, &exch);
+    if (!m->sharded()) lo = 1 - (int)m->j0, hi = (int)m->g.ny - 1 - (int)m->j0;
+    int pad = 0, occ = 0, nwc = 0, nseg = 0;
+    lds_geometry8(m->g, lo, hi, persist != 0, &pad, &occ, &nwc, &nseg);
+    if (lds_pad) *lds_pad = pad;
+    if (wgs_per_cu) *wgs_per_cu = occ;
+    if (wave_cols) *wave_cols = nwc;
+    if (segments) *segments = nseg;
     return 0;
 }
 

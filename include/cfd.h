@@ -49,10 +49,14 @@ typedef enum {
                             the reference has none): cfd_update refuses to step on
                             and cfd_get_residuals reports it (filling *out all the
                             same) until cfd_set_state injects a new state */
-    CFD_ETIMEOUT = -6, /* the persistent Jacobi solve (CFD_PERSIST=1) gave up waiting for a
-                          neighbouring workgroup (they were not all resident): that
-                          solve's p' is invalid; the model falls back to one launch
-                          per block from then on */
+    CFD_ETIMEOUT = -6, /* a persistent Jacobi solve (CFD_PERSIST=1) waited past its
+                          deadline (CFD_PERSIST_DEADLINE_US, default 10 s) for a
+                          neighbouring tile: a fault, not a residency effect (since r4
+                          the ticketed launch completes with any number of its
+                          workgroups resident, beside any other kernel).  That solve's
+                          p', and the steps enqueued after it, are invalid: restore a
+                          checkpoint (cfd_get_state / cfd_set_state); the model runs
+                          its solves one launch per block from then on */
 } cfd_status;
 
 typedef struct cfd_model cfd_model;
@@ -77,10 +81,16 @@ enum { CFD_INLET_UNIFORM = 0, CFD_INLET_PARABOLIC = 1 };
  * :775-795 + :1344-1470): p' restarts from 0 each solve, arithmetic in double
  * with f32 storage as in the script; SOR is swept red-black (omega 1.7,
  * jacobi_iters iterations, early exit at p_tol); MULTIGRID runs 3 V-cycles and
- * reports max |A p' - rhs|.  Both run on sharded models too: SOR per slab
- * with a 2-row p' exchange per iteration (>= 16 interior rows and halo depth
- * >= 2 per slab), MULTIGRID by gathering the rhs and solving the whole grid on
- * every rank (bit-identical to the unsharded solve). */
+ * reports max |A p' - rhs|.  Both run on sharded models too (>= 16 interior
+ * rows and halo depth >= 2 per slab), bit-identical to the unsharded solve.
+ * SOR, fixed count (tol_enabled 0): deep ghosts -- an hg-row p' exchange
+ * every hg/2 iterations, the iterations between recomputing shrinking ghost
+ * bands; with the tolerance on, a 2-row exchange and an all-reduced residual
+ * per iteration (checked one iteration behind).  MULTIGRID: the fine levels
+ * whose every slab boundary divides by 2^(l+1) (>= 16 rows per slab there)
+ * are partitioned -- each rank smooths, forms residuals and restricts only
+ * its rows, with 8-row ghost exchanges per level -- and the coarser levels
+ * are gathered and solved whole on every rank. */
 enum { CFD_SOLVER_JACOBI = 0, CFD_SOLVER_SOR = 1, CFD_SOLVER_MULTIGRID = 2 };
 enum { CFD_BC_CHANNEL = 0, CFD_BC_CAVITY = 1 };
 typedef struct {
@@ -209,6 +219,10 @@ int cfd_timing_end(cfd_model *m, double *solve_ms, uint64_t *sweeps, double *ste
  * last window (0 when a phase was not timed). */
 int cfd_timing_phases(cfd_model *m, int on);
 int cfd_timing_phase_ms(const cfd_model *m, double *predict_ms, double *finish_ms);
+/* Sharded models over RCCL, same windows: the summed duration of every halo
+ * exchange group and all-reduce on the stream it runs on (waiting for the
+ * peer included), and how many there were.  (new; per-rank exchange time) */
+int cfd_timing_exchange_ms(const cfd_model *m, double *exchange_ms, uint64_t *exchanges);
 /* p' halo depth (rows exchanged per RCCL round) of a sharded model. */
 int cfd_get_halo_depth(const cfd_model *m);
 /* Jacobi kernel configuration chosen at creation: division form proven exact
@@ -227,6 +241,13 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
  * Blocks after them (shorter ones of an uneven split) are k_jacobi_lds
  * launches of their own. */
 int cfd_get_persist_blocks(const cfd_model *m, int *blocks);
+/* The tile geometry of the model's 8-sweep kind-5 Jacobi launch over its
+ * first block's rows (persist != 0: the persistent form's): the dynamic LDS
+ * pad in bytes (24 KiB caps a CU at 3 four-wave workgroups on cache-resident
+ * slabs), the workgroups per CU the round is sized for, the wave columns and
+ * the wave segments per column.  (new; diagnostics) */
+int cfd_get_jacobi_geometry(const cfd_model *m, int persist, int *lds_pad, int *wgs_per_cu,
+                            int *wave_cols, int *segments);
 
 /* Host-only slab plan used by cfd_create_sharded (no device needed; the
  * multi-rank CPU tests drive the same plan):

@@ -71,3 +71,36 @@ def test_bench_gpus_n_never_reports_fewer_ranks():
     assert p.returncode != 0
     assert not any(l.get("n_gpus") == 1 for l in lines)
     assert "needs 2 GPUs" in p.stderr
+
+
+def test_assemble_slabs_owned_rows_and_shared_v_face():
+    """cfdamd.assemble_slabs (bench.py's N > 1 parity step gathers with it):
+    owned rows concatenate; the v face row j1 both neighbours hold comes once,
+    and a mismatch between the two copies is an error, not a silent pick."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "cfd-demo_amd"))
+    import cfdamd
+    nx, ny = 8, 10
+    rng = np.random.default_rng(3)
+    g = {f: rng.standard_normal(n).astype(np.float32) for f, n in
+         (("u", (nx + 1) * ny), ("p", nx * ny), ("p_prime", nx * ny), ("u_star", (nx + 1) * ny),
+          ("rhs", nx * ny), ("v", nx * (ny + 1)), ("v_star", nx * (ny + 1)))}
+    cuts = [0, 3, 7, 10]
+    slabs = []
+    for j0, j1 in zip(cuts[:-1], cuts[1:]):
+        st = {f: g[f].reshape(-1, nx + 1)[j0:j1].ravel() for f in ("u", "u_star")}
+        st.update({f: g[f].reshape(-1, nx)[j0:j1].ravel() for f in ("p", "p_prime", "rhs")})
+        st.update({f: g[f].reshape(-1, nx)[j0:j1 + 1].ravel() for f in ("v", "v_star")})
+        slabs.append((j0, j1, st))
+    out = cfdamd.assemble_slabs(slabs, nx)
+    for f in g:
+        assert np.array_equal(out[f], g[f]), f
+    slabs[1][2]["v"] = slabs[1][2]["v"].copy()
+    slabs[1][2]["v"][-nx] += 1.0   # slab 1's copy of face row 7 differs from slab 2's
+    try:
+        cfdamd.assemble_slabs(slabs, nx)
+    except ValueError as e:
+        assert "face row 7" in str(e)
+    else:
+        raise AssertionError("a differing shared face row must raise")

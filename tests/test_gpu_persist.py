@@ -1,11 +1,15 @@
 """GPU: the persistent fixed-count solve (k_jacobi_persist, CFD_PERSIST=1).
 
-One launch runs all but the last 8-sweep block of a solve; workgroups hand
-rows to their neighbours through per-workgroup flags inside the launch
-(write-through p' stores, L1-bypassing loads).  Every field must equal the
-per-launch form bit for bit -- across grids whose tiles split unevenly, with
-the obstacle masks, the second-order scheme, corrector passes, the IEEE
-division path, and a developed 4096^2 state -- and the oracle.
+One launch runs the 8-sweep blocks of a solve; workgroups take (block, tile)
+tasks by ticket and hand rows to their neighbours through per-tile flags
+inside the launch (write-through p' stores, agent acquire after each poll).
+Every field must equal the per-launch form bit for bit -- across grids whose
+tiles split unevenly, with the obstacle masks, the second-order scheme,
+corrector passes, the IEEE division path, and a developed 4096^2 state -- and
+the oracle; every persistent case asserts that the persistent path ran.
+Since r4 the launch completes with any number of its workgroups resident:
+grids smaller and larger than one round, and two models' launches running
+at once on one GPU, are bitwise too.
 """
 import numpy as np
 import pytest
@@ -17,40 +21,70 @@ pytestmark = pytest.mark.gpu
 STATE = ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
 
 
-def _states(monkeypatch, grid, params, steps, develop=0):
+def pow2_grid(nx, ny, inv=512):
+    """A cavity-type grid whose spacings are 1/inv (a power of two) whatever
+    nx, ny are: the reciprocal-multiply division is proven exact there, so
+    the default kernel is kind 5 and fixed-count solves run persistently
+    (cavity_grid(nx, ny) has spacing 1/ny, which for ny = 200, 384, 1000 gives
+    IEEE division, kind 4 and no persistent launch)."""
+    import cfdamd
+    return cfdamd.Grid(nx, ny, nx / inv, ny / inv, None)
+
+
+def _states(monkeypatch, grid, params, steps, develop=0, envs=("0", "1"), persistent=True):
+    """States after `steps` steps with CFD_PERSIST=0 then =1 (or `envs`: a
+    list of CFD_PERSIST values or dicts of variables); asserts which path each
+    solve took (persist_blocks 0 per launch, > 0 persistent -- or 0 when
+    `persistent` is False: a solve with fewer than two leading 8-sweep blocks
+    has nothing to run persistently)."""
     import cfdamd
     out = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("CFD_PERSIST", env)
+    for env in envs:
+        env = env if isinstance(env, dict) else {"CFD_PERSIST": env}
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         m = cfdamd.Model(grid, params, device=0)
         try:
             if develop:
                 m.update_n(develop)
             m.update_n(steps)
-            out.append(m.get_state())
+            st = m.get_state()
+            pb = m.persist_blocks
+            if env.get("CFD_PERSIST", "1") == "0" or not persistent:
+                assert pb == 0, (env, pb)
+            else:
+                assert pb > 0, (env, pb)
+            out.append(st)
         finally:
             m.close()
     return out
 
 
-@pytest.mark.parametrize("nx,ny,iters", [(256, 200, 50), (1024, 1024, 100), (640, 1000, 200), (1024, 1024, 1200),
-                                          (2048, 384, 40)])
+@pytest.mark.parametrize("nx,ny,iters", [(256, 200, 50), (256, 200, 48), (1024, 1024, 100), (640, 1000, 200),
+                                          (1024, 1024, 1200), (2048, 384, 40)])
 def test_persist_matches_launches_cavity(monkeypatch, nx, ny, iters):
+    """50 sweeps split 8 + 6 x 7 (one leading 8-sweep block: per launch);
+    100 = 9 x 8 + 4 x 7 (9 persistent blocks, the 7-sweep ones per launch)."""
     import cfdamd
     params = cfdamd.SimulationParams.cavity(400.0, iters, corrector_passes=0, tol_enabled=False)
-    a, b = _states(monkeypatch, cfdamd.cavity_grid(nx, ny), params, 12)
+    a, b = _states(monkeypatch, pow2_grid(nx, ny), params, 12, persistent=iters != 50)
     for f in STATE:
         assert_bitwise(f"persist cavity {nx}x{ny}:{f}", b[f], a[f])
 
 
-def test_persist_matches_launches_channel_so_passes(monkeypatch):
+@pytest.mark.parametrize("kind", ["5", "default"])
+def test_persist_matches_launches_channel_so_passes(monkeypatch, kind):
     """Channel with a cylinder (masks), second order, 3 corrector passes
-    (each pass's solve is persistent), non-power-of-two spacing."""
+    (each pass's solve is persistent), non-power-of-two spacing: kind 5 forced
+    (CFD_TB_KIND=5), so the persistent launch runs its IEEE / FMA-corrected
+    division instantiation; by default such grids run kind 4 per launch."""
     import cfdamd
     grid = cfdamd.Grid(800, 264, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5))
     params = cfdamd.SimulationParams(velocity_scheme=cfdamd.VelocityScheme.SecondOrder,
                                      jacobi_iters=64, corrector_passes=3, tol_enabled=False)
-    a, b = _states(monkeypatch, grid, params, 10)
+    if kind == "5":
+        monkeypatch.setenv("CFD_TB_KIND", "5")
+    a, b = _states(monkeypatch, grid, params, 10, persistent=kind == "5")
     for f in STATE:
         assert_bitwise(f"persist channel:{f}", b[f], a[f])
 
@@ -80,8 +114,112 @@ def test_persist_matches_oracle(monkeypatch):
             m.update()
             o.update()
         st = m.get_state()
+        assert m.persist_blocks == 6, m.persist_blocks
         for f in STATE:
             assert_bitwise(f"persist oracle:{f}", st[f], o.field(f))
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("nwg", ["1", "7", "5000"])
+def test_persist_any_grid_size(monkeypatch, nwg):
+    """CFD_PERSIST_GRID: the launch's workgroups take the (block, tile) tasks
+    by ticket, so it completes with one workgroup, with fewer workgroups than
+    tiles (later tiles of block 0 start as workgroups free up), and with more
+    than the GPU holds at once (the surplus starts late and finds the tickets
+    gone) -- the r3 launch needed exactly one resident round.  Bitwise vs
+    per launch."""
+    import cfdamd
+    params = cfdamd.SimulationParams.cavity(400.0, 64, corrector_passes=0, tol_enabled=False)
+    a, b = _states(monkeypatch, pow2_grid(640, 1000), params, 4,
+                   envs=("0", {"CFD_PERSIST": "1", "CFD_PERSIST_GRID": nwg}))
+    for f in STATE:
+        assert_bitwise(f"persist grid {nwg}:{f}", b[f], a[f])
+
+
+@pytest.mark.timeout(300)
+def test_persist_two_models_at_once(monkeypatch):
+    """Two models on one GPU step at the same time, each on its own stream
+    from its own thread, with persistent solves and no gate between them
+    (the co-tenant case that stranded the r3 launch until its spin limit):
+    each equals its per-launch run bit for bit."""
+    import threading
+    import cfdamd
+    grids = (cfdamd.cavity_grid(1024, 1024), pow2_grid(768, 1536))
+    params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
+    monkeypatch.setenv("CFD_PERSIST", "0")
+    want = []
+    for g in grids:
+        m = cfdamd.Model(g, params, device=0)
+        try:
+            m.update_n(8)
+            want.append(m.get_state())
+        finally:
+            m.close()
+    monkeypatch.setenv("CFD_PERSIST", "1")
+    monkeypatch.setenv("CFD_PERSIST_GATE", "0")
+    models = [cfdamd.Model(g, params, device=0) for g in grids]
+    got, errors = [None, None], []
+
+    def run(k):
+        try:
+            for _ in range(8):   # one step per call: the two streams interleave
+                models[k].update()
+            got[k] = (models[k].get_state(), models[k].persist_blocks)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    try:
+        ts = [threading.Thread(target=run, args=(k,), daemon=True) for k in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(240)
+    finally:
+        for m in models:
+            m.close()
+    assert not errors, errors
+    for k in range(2):
+        assert got[k][1] == 25, got[k][1]
+        for f in STATE:
+            assert_bitwise(f"two models [{k}]:{f}", got[k][0][f], want[k][f])
+
+
+def test_persist_deadline_fault_is_loud_and_recoverable(monkeypatch):
+    """A wait past the deadline (forced here: CFD_PERSIST_DEADLINE_US=0, so
+    any neighbour not yet done counts as a fault) aborts the launch: the next
+    call raises CFD_ETIMEOUT, the model's later solves run per launch, and the
+    caller's checkpoint (cfd_get_state / cfd_set_state) restores a state from
+    which the steps equal the oracle."""
+    import cfdamd
+    from cfdamd._lib import CFD_ETIMEOUT, CfdError
+    from oracle import OracleModel
+    grid = cfdamd.cavity_grid(1024, 1024)
+    params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
+    o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly, bc_kind=1, viscosity=1.0 / 400.0,
+                    jacobi_iters=200, tol_enabled=False, corrector_passes=0)
+    monkeypatch.setenv("CFD_PERSIST", "1")
+    m = cfdamd.Model(grid, params, device=0)
+    try:
+        for _ in range(3):
+            m.update()
+            o.update()
+        ckpt = m.get_state()
+        monkeypatch.setenv("CFD_PERSIST_DEADLINE_US", "0")
+        with pytest.raises(CfdError) as ei:
+            for _ in range(20):   # a fault on the first persistent solve is near-certain
+                m.update()
+                m.synchronize()
+        assert ei.value.code == CFD_ETIMEOUT, ei.value
+        monkeypatch.delenv("CFD_PERSIST_DEADLINE_US")
+        m.set_state(**ckpt)
+        for _ in range(2):
+            m.update()
+            o.update()
+        st = m.get_state()
+        assert m.persist_blocks == 0   # per launch after the fault
+        for f in STATE:
+            assert_bitwise(f"after deadline fault:{f}", st[f], o.field(f))
     finally:
         m.close()
 
@@ -91,7 +229,7 @@ def test_persist_off_under_graph_replay(monkeypatch):
     the captured solves run per launch (a replayed persistent launch would
     reuse its flag epoch); the replay equals the eager persistent run."""
     import cfdamd
-    grid = cfdamd.cavity_grid(512, 384)
+    grid = pow2_grid(512, 384)
     params = cfdamd.SimulationParams.cavity(400.0, 64, corrector_passes=0, tol_enabled=False)
     states = []
     for graph in ("0", "1"):
@@ -161,8 +299,9 @@ def test_persist_runs_between_exchanges_on_slabs(monkeypatch, n):
 def test_kind5_fields_over_1GiB(monkeypatch):
     """A single-domain grid whose p' field exceeds 1 GiB (16384 x 17408,
     1.14 GiB per field): kind 5 -- per-wave buffer windows, so a parked
-    lane's offset never wraps -- runs it (persistently) and equals kind 1
-    (CFD_TB_KIND=1, the former fallback) bit for bit."""
+    lane's offset never wraps -- runs it persistently (4,410 tiles, more
+    than one round of workgroups) and equals kind 1 (CFD_TB_KIND=1, the
+    former fallback) bit for bit."""
     import cfdamd
     grid = cfdamd.cavity_grid(16384, 17408)
     params = cfdamd.SimulationParams.cavity(1000.0, 16, corrector_passes=0, tol_enabled=False)
@@ -174,6 +313,8 @@ def test_kind5_fields_over_1GiB(monkeypatch):
             assert m.jacobi_kernel["kind"] == int(kind), m.jacobi_kernel
             m.update_n(8)   # past the inlet ramp's first steps: p' non-zero under the lid
             st = m.get_state()
+            if kind == "5":
+                assert m.persist_blocks == 2, m.persist_blocks
             states.append({f: st[f] for f in ("u", "v", "p_prime", "rhs")})
             del st
         finally:

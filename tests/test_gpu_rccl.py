@@ -6,7 +6,9 @@ box: each rank gets its own NCCL_HOSTID, so RCCL connects them through its
 socket transport over loopback instead of refusing two ranks on one device
 (tools/rccl_loopback.py).  The gathered slabs must equal the single-domain
 model bit for bit, in the bench's fixed-count mode (deep halos, overlapped
-band exchange) and in the reference's tolerance mode (lagged convergence)."""
+band exchange, persistent runs between exchanges -- since r4 with the ranks'
+kernels sharing the GPU) and in the reference's tolerance mode (lagged
+convergence)."""
 import json
 import os
 import subprocess
@@ -87,6 +89,16 @@ def test_bench_self_launch_two_ranks_loopback():
     assert r.returncode == 0 and len(lines) == 1, (r.stdout[-2000:], r.stderr[-3000:])
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2, lines[0]
     assert lines[0]["launcher"] == "bench.py" and len(lines[0]["rank_ms_per_step"]) == 2
+    # r4: the N > 1 line verifies itself -- one more step on the slabs equals
+    # a single-domain model's step from the gathered state -- and carries
+    # every rank's phase and RCCL exchange times and its Jacobi geometry
+    out = lines[0]
+    assert out["parity_sharded_step"] is True, out.get("parity_sharded_step_detail")
+    assert len(out["rank_phases"]) == 2, out["rank_phases"]
+    for rp in out["rank_phases"]:
+        assert rp["exchange_us_per_step"] > 0 and rp["exchanges_per_step"] >= 3, rp
+        assert rp["geometry"]["wave_cols"] > 0, rp
+    assert out["jacobi_geometry"]["segments"] > 0
 
 
 @pytest.mark.timeout(600)
@@ -108,3 +120,6 @@ def test_rccl_developed_full_size_slabs_bitwise(n, nx, ny):
         assert x["bitwise_equal_single_domain"], x
         assert x["ranks_seen"] == n
         assert x["boundary_pprime_nonzero_frac"] >= 0.9, x
+        # persistent runs between the p' exchanges, beside the other ranks'
+        # kernels on the shared GPU: the SCALE configuration (r4)
+        assert x["persist_blocks"] >= 2, x

@@ -15,7 +15,9 @@ from _util import assert_bitwise
 pytestmark = pytest.mark.gpu
 
 
-def run_sharded(n, grid, params, steps, halo_depth):
+def run_sharded(n, grid, params, steps, halo_depth, geoms=None):
+    """geoms: a list that receives every slab's Jacobi tile geometry
+    (Model.jacobi_geometry, persistent form)."""
     import cfdamd
     if halo_depth is not None:   # None: the library's default depth (bench.py's)
         os.environ["CFD_HALO_DEPTH"] = str(halo_depth)
@@ -26,6 +28,8 @@ def run_sharded(n, grid, params, steps, halo_depth):
         try:
             m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=r, local_hub=hub)
             models[r] = m
+            if geoms is not None:
+                geoms.append(m.jacobi_geometry())
             for _ in range(steps):
                 m.update()
             m.synchronize()
@@ -154,8 +158,20 @@ def test_sharded_bench_geometry_matches_single_domain(n, nx, ny, steps):
     import cfdamd
     grid = cfdamd.cavity_grid(nx, ny)
     params = cfdamd.SimulationParams.cavity(1000.0, 200, corrector_passes=0, tol_enabled=False)
-    st = run_sharded(n, grid, params, steps, None)
+    geoms = []
+    st = run_sharded(n, grid, params, steps, None, geoms)
     assert all(s[3] == 32 for s in st), [s[3] for s in st]
+    # one Jacobi geometry along the weak-scaling series (r4): every slab runs
+    # the padded 3-workgroups-per-CU round of the single-domain 4096^2 model
+    # (keyed on owned rows; the C5 slab's 32 ghost rows used to tip it over)
+    c3 = cfdamd.Model(cfdamd.cavity_grid(4096), params, device=0)
+    try:
+        want = c3.jacobi_geometry()
+    finally:
+        c3.close()
+    assert want["lds_pad"] == 24 * 1024, want
+    for gm in geoms:
+        assert (gm["lds_pad"], gm["wgs_per_cu"]) == (want["lds_pad"], want["wgs_per_cu"]), (gm, want)
     got = assemble(st, nx)
     del st
     m = cfdamd.Model(grid, params, device=0)

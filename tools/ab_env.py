@@ -25,6 +25,8 @@ for rnd in range(3):
         d = json.loads(out.stdout.strip().splitlines()[-1])
         key = "us_per_sweep" if "us_per_sweep" in d else "ms_per_step"
         print(json.dumps({"setting": sp, "round": rnd, "us_per_sweep": d.get("us_per_sweep"),
-                          "ms_per_step": round(d["ms_per_step"], 4)}), flush=True)
+                          "ms_per_step": round(d["ms_per_step"], 4),
+                          "geometry": d.get("geometry"), "persist_blocks": d.get("persist_blocks"),
+                          "crc": d.get("state_crc32")}), flush=True)
         best[sp] = min(best.get(sp, 1e9), d[key])
 print(json.dumps({"best_" + key: best}), flush=True)
