@@ -441,6 +441,14 @@ class Model:
                     segments=v[3].value)
 
     @property
+    def persist_steals(self) -> int:
+        """Persistent-solve blocks run by a workgroup other than the tile's
+        owner (cfd_get_persist_steals; 0 when every owner was resident)."""
+        n = C.c_uint64()
+        check("cfd_get_persist_steals", load().cfd_get_persist_steals(self._hh(), C.byref(n)))
+        return int(n.value)
+
+    @property
     def persist_blocks(self) -> int:
         """8-sweep blocks the last fixed-count solve ran in one persistent
         launch (k_jacobi_persist); 0 when every block had its own launch."""

@@ -36,10 +36,10 @@ constexpr int kMaxPasses = 64;     // corrector passes + 1
 constexpr int kResSlots = 32;
 constexpr int kResStride = 16;
 // persistent-solve words (k_jacobi_persist), one 64-B line each: line 0 [1]
-// the abort flag; lines 1 and 2 the task tickets of even / odd epochs; then
-// one hand-off flag per tile
+// the abort flag, [2] the blocks stolen so far; then one line per tile: [0]
+// its done flag, [1] its claim counter
 constexpr int kPersistFlagStride = 16;
-constexpr int kPersistHeadLines = 3;
+constexpr int kPersistHeadLines = 1;
 // flag = epoch << kPersistBlockBits | blocks done: room for every block of the
 // longest solve (kMaxSweeps / 8 = 512), epochs below 2^(32 - bits)
 constexpr int kPersistBlockBits = 10;

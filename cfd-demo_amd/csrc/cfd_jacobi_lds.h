@@ -562,23 +562,37 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 
 // Persistent fixed-count solve: ONE launch runs nblk blocks of T sweeps
 // (par0.. launches of the per-launch form) over ntiles tiles (tile = the four
-// wave segments of one workgroup of the per-launch form).  The work is
-// nblk * ntiles tasks (block b, tile t), numbered block-major; workgroups take
-// task tickets IN ORDER from one counter (a returning atomic, fetched one task
-// ahead) until the tickets run out.  Task (b, t) reads the rows that tile t
-// and its 3 x 3 neighbours (adjacent wave columns hold the halo lanes'
-// columns, adjacent row groups the T-row input bands) wrote in block b-1, and
-// overwrites the buffer they read in block b-1, so it starts once all nine
-// have finished block b-1 — no launch boundary, no grid-wide drain, and a slow
-// task holds back only its neighbours.
+// wave segments of one workgroup of the per-launch form).  Task (t, b), block
+// b of tile t, reads the rows that t and its 3 x 3 neighbours (adjacent wave
+// columns hold the halo lanes' columns, adjacent row groups the T-row input
+// bands) wrote in block b-1, and overwrites the buffer they read in block
+// b-1, so it starts once all nine have finished block b-1 — no launch
+// boundary, no grid-wide drain, and a slow tile holds back only its
+// neighbours.
 //
-// Why tickets: every task a waiting workgroup depends on has a smaller
-// ticket, so it was taken by a workgroup that is running, and (by induction)
-// it finishes.  The launch therefore completes whatever number of its
-// workgroups the GPU holds at once — a co-tenant kernel, another model's
-// stream, RCCL kernels or a grid larger than one round only slow it down.
-// (The r3 form bound tile w to workgroup w and needed all of them resident:
-// a co-tenant could strand it until its spin limit, with p' left invalid.)
+// Ownership with stealing.  Workgroup w owns tile w (XCD-renumbered, as the
+// per-launch form maps it) and runs its blocks in order, so on a GPU that
+// holds every workgroup at once each one keeps its tile (and its rows' L2) for
+// the whole solve.  A block is CLAIMED before it runs: tile t's line holds a
+// claim counter beside its done flag, advanced by compare-and-swap, so every
+// task runs exactly once.  An owner claims all its tile's unclaimed blocks
+// with one CAS when it starts (no atomic per block on the fast path).  A
+// workgroup that has waited more than `steal` ticks for a
+// neighbour's block b-1 that nobody has claimed — its owner is not resident
+// (a co-tenant kernel, another model's launch, RCCL kernels, a grid larger
+// than the GPU holds) — claims that block itself, runs it when ready and then
+// returns to its own task (a small stack of claimed tasks in LDS).
+// Deadlock-free by construction: a wait is on a block that is either claimed
+// by a running workgroup or stealable; the owner's own task sits at the
+// bottom of its stack and a thief takes only a block below the one it waits
+// to run (one CAS from the value it read, never "the next one"), so blocks
+// fall strictly up every stack, no task depends on one below it, and waits
+// never form a cycle.  The launch completes with any number of its workgroups resident.
+// (The r3 form needed all of them resident at once: a co-tenant could strand
+// it until its spin limit, with p' left invalid; a ticketed form that took
+// tasks in block order measured 7.6 us per sweep against 4.7: a workgroup
+// then waits for an arbitrary tile's neighbourhood, in effect a grid barrier
+// per block.)
 //
 // Hand-off (MI355X_MICROARCH.md "Valid forms", Consumer, always): p' stores
 // write through (sc1) and every wave drains them (s_waitcnt vmcnt(0)) before
@@ -587,94 +601,188 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 // s_sleep), then ONE agent acquire (buffer_inv sc1) + vmcnt(0) + the
 // workgroup barrier before any p' load.  The launch runs several workgroups
 // per CU, outside the table under which sc1 loads alone may replace the
-// acquire, so the acquire stays (acq = 1, CFD_PERSIST_ACQ=0 opts out for
-// measurement only).  Flags hold epoch * 2^kPersistBlockBits + blocks done (a
-// solve has at most kMaxSweeps / 8 = 512 blocks); the host gives every
-// persistent launch a new epoch (never under graph capture: arguments would
-// freeze), so flags never need clearing between launches; launch e zeroes
-// the ticket counter of launch e+1 (the two alternate by epoch parity).
-// Waits are bounded by wall time (s_memrealtime, `deadline` ticks of 10 ns):
-// past it the waiter sets the abort word persist[1], every workgroup leaves
-// at its next poll or at entry, and a zero-copy host word makes the model's
-// next cfd_* call report CFD_ETIMEOUT (a fault, not a residency effect).
+// acquire, so the acquire stays (acq = 1; CFD_PERSIST_ACQ=0 opts out for
+// measurement only).  Flags and claim counters hold epoch * 2^kPersistBlockBits
+// + blocks done / claimed (a solve has at most kMaxSweeps / 8 = 512 blocks);
+// the host gives every persistent launch a new epoch (never under graph
+// capture: arguments would freeze), so a value below the epoch's base reads
+// as 0 and nothing needs clearing between launches.  Waits are bounded by
+// wall time (s_memrealtime, `deadline` ticks of 10 ns): past it the waiter
+// sets the abort word persist[1], every workgroup leaves at its next poll or
+// at entry, and a zero-copy host word makes the model's next cfd_* call report
+// CFD_ETIMEOUT (a fault: residency no longer causes one).
+constexpr int kStealDepth = 16;
 template <int T, int FAST>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_persist(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *persist, uint32_t *host_fail, uint32_t *res_slots, uint32_t epoch, int pass,
     int par0, int nblk, int out_lo, int out_hi, int nwc, int nseg, int wlo, int whi, int ngrp,
-    int acq, uint32_t deadline) {
+    int acq, uint32_t deadline, uint32_t steal, int late) {
     using M = LdsMarch<T, FAST, 4>;
     __shared__ f2 lds[kLdsWaves * M::D * 64];
-    // task_s[i & 1]: the ticket of the workgroup's task i (double-buffered: a
-    // wave may still read entry i after the barrier while entry i+1 is written)
-    __shared__ int task_s[2], abort_s;
-    uint32_t *tickets = persist + (1 + (epoch & 1)) * kPersistFlagStride;
-    if (blockIdx.x == 0 && threadIdx.x == 0)   // the next launch's counter (stream-ordered)
-        __hip_atomic_store(persist + (1 + ((epoch + 1) & 1)) * kPersistFlagStride, 0u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // control (wave 0 writes, everyone reads after a barrier): the task to
+    // run, the claimed-task stack, the owner's next claimed block
+    // (-2: claim it now, -1: none left)
+    __shared__ int run_tile_s, run_blk_s, abort_s, own_next_s, sp_s;
+    __shared__ int stk_tile[kStealDepth], stk_blk[kStealDepth];
     if (pass_off(ctl, pass)) return;
+    const int ntiles = ngrp * nwc;
+    const int own = xcd_block(g);
+    if (own >= ntiles) return;   // a grid larger than the tiles: nothing owned
     const unsigned base = epoch << kPersistBlockBits;
-    uint32_t *flags = persist + kPersistHeadLines * kPersistFlagStride;
-    const int ntiles = ngrp * nwc, ntask = nblk * ntiles;
+    uint32_t *lines = persist + kPersistHeadLines * kPersistFlagStride;   // per tile: [0] done, [1] claimed
     const int lane = (int)threadIdx.x & 63;
-    constexpr int kTicketThread = (kLdsWaves - 1) * 64;   // the last wave fetches tickets (wave 0 polls)
+    // blocks claimed of a tile from its claim word (values of older epochs read 0)
+    auto count = [&](unsigned v) -> int { return v < base ? 0 : (int)(v - base); };
+    // claim blocks of tile t by CAS from `v` (a read or guess of its claim
+    // word): the first block claimed, or -1 when every block is claimed or
+    // (thief) the word was not `v`.  all = true (the owner, once, when it
+    // starts): every block not yet claimed, retrying from the word's actual
+    // value -- a resident owner thus holds its whole tile and no thief ever
+    // touches it, with no atomic per block.  A thief (all = false) takes
+    // exactly the one block it saw unclaimed, or nothing: a later block of
+    // that tile could depend on a task the thief holds below it on its stack
+    // (a cycle).
+    auto claim = [&](int t, unsigned v, bool all) -> int {
+        uint32_t *w = lines + (size_t)t * kPersistFlagStride + 1;
+        for (;;) {
+            const int c = count(v);
+            if (c >= nblk) return -1;
+            unsigned exp = v;
+            if (__hip_atomic_compare_exchange_strong(w, &exp, base + (unsigned)(all ? nblk : c + 1),
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                return c;
+            if (!all) return -1;
+            v = exp;   // the word as it was: retry from it
+        }
+    };
     if (threadIdx.x == 0) {
+        sp_s = 0;
+        own_next_s = -2;
         // fail fast after an abort (every later launch of the model too)
-        const bool dead = __hip_atomic_load(persist + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-        task_s[0] = dead ? ntask : (int)__hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT);
+        abort_s = __hip_atomic_load(persist + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        if (late > 0 && own % late == 1) {   // test knob: this owner starts late (not resident)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < 200000u) __builtin_amdgcn_s_sleep(127);
+        }
     }
     __syncthreads();
-    int t = task_s[0];
-    for (int i = 1; t < ntask; ++i) {
-        const int b = t / ntiles, tile = t - b * ntiles;
-        if (b > 0) {
-            if (threadIdx.x < 64) {
-                // lanes 0..8 watch the tile and its neighbours, lane 9 the abort word
-                const int wc = tile % nwc, gi = tile / nwc;
+    if (abort_s) return;
+    for (;;) {
+        if (threadIdx.x < 64) {
+            // ---- wave 0: the next task that is ready (claiming / stealing) ----
+            int sp = sp_s, run_t = -1, run_b = -1;
+            bool fail = false;
+            if (sp == 0) {
+                int nb = own_next_s;
+                if (nb == -2) {
+                    int c = -1;
+                    if (lane == 0) c = claim(own, 0u, true);
+                    nb = __builtin_amdgcn_readfirstlane(c);
+                }
+                if (nb >= 0) {
+                    if (lane == 0) {
+                        stk_tile[0] = own;
+                        stk_blk[0] = nb;
+                    }
+                    sp = 1;
+                }
+                own_next_s = -1;
+            }
+            while (sp > 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // stack writes before reads
+                const int tt = stk_tile[sp - 1], bb = stk_blk[sp - 1];
+                if (bb == 0) {
+                    run_t = tt, run_b = bb;
+                    --sp;
+                    break;
+                }
+                // lanes 0..8 watch the task's tile and its neighbours, lane 9 the abort word
+                const int wc = tt % nwc, gi = tt / nwc;
                 const int c = wc + lane % 3 - 1, r = gi + lane / 3 - 1;
-                const uint32_t *w = lane < 9 ? (c >= 0 && c < nwc && r >= 0 && r < ngrp
-                                                    ? flags + (size_t)(r * nwc + c) * kPersistFlagStride
-                                                    : nullptr)
-                                             : (lane == 9 ? persist + 1 : nullptr);
-                const unsigned want = base + (unsigned)b;
+                const bool nbr = lane < 9 && c >= 0 && c < nwc && r >= 0 && r < ngrp;
+                const int nt = nbr ? r * nwc + c : -1;
+                const uint32_t *w = nbr ? lines + (size_t)nt * kPersistFlagStride
+                                        : (lane == 9 ? persist + 1 : nullptr);
+                const unsigned want = base + (unsigned)bb;
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                bool fail = false;
+                bool ready = false, pushed = false;
                 for (;;) {
                     const unsigned v = w ? __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                          : 0u;
-                    const bool ok = lane < 9 ? (w == nullptr || v >= want) : v == 0u;
-                    if (__all(ok)) break;
-                    if (__any(lane == 9 && v != 0u) ||
-                        __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)deadline) {
+                    const bool ok = lane < 9 ? (!nbr || v >= want) : v == 0u;
+                    if (__all(ok)) {
+                        ready = true;
+                        break;
+                    }
+                    const uint64_t el = __builtin_amdgcn_s_memrealtime() - t0;
+                    if (__any(lane == 9 && v != 0u) || el > (uint64_t)deadline) {
                         fail = true;
                         break;
                     }
+                    if (el > (uint64_t)steal && sp < kStealDepth) {
+                        // a neighbour block this task needs that nobody has claimed
+                        const unsigned cw = nbr && v < want
+                                                ? __hip_atomic_load(w + 1, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                                : 0u;
+                        const bool cand = nbr && v < want && count(cw) < bb;
+                        const uint64_t m = __ballot(cand);
+                        if (m) {
+                            const int l = __builtin_ctzll(m);
+                            const int st = __shfl(nt, l, 64);
+                            const unsigned sv = __shfl(cw, l, 64);
+                            int got = -1;
+                            if (lane == 0) {
+                                got = claim(st, sv, false);
+                                if (got >= 0)   // steals counted for diagnostics (cfd_get_persist_steals)
+                                    __hip_atomic_fetch_add(persist + 2, 1u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                            got = __builtin_amdgcn_readfirstlane(got);
+                            if (got >= 0) {   // run it first, then come back to this task
+                                if (lane == 0) {
+                                    stk_tile[sp] = st;
+                                    stk_blk[sp] = got;
+                                }
+                                ++sp;
+                                pushed = true;
+                                break;
+                            }
+                        }
+                    }
                     __builtin_amdgcn_s_sleep(2);
                 }
-                if (lane == 0) {
-                    abort_s = fail;
-                    if (fail) {
-                        __hip_atomic_store(persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (host_fail)   // zero-copy host word: cfd_* calls report CFD_ETIMEOUT
-                            __hip_atomic_store(host_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (fail) break;
+                if (pushed) continue;
+                if (ready) {
+                    run_t = tt, run_b = bb;
+                    --sp;
+                    if (acq) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    } else {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps loads below the poll
                     }
-                }
-                if (acq) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                } else {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps loads below the poll
+                    break;
                 }
             }
-            __syncthreads();
-            if (abort_s) return;   // workgroup-uniform
+            if (lane == 0) {
+                sp_s = sp;
+                run_tile_s = run_t;
+                run_blk_s = run_b;
+                abort_s = fail;
+                if (fail) {
+                    __hip_atomic_store(persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (host_fail)   // zero-copy host word: cfd_* calls report CFD_ETIMEOUT
+                        __hip_atomic_store(host_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         }
-        // the next ticket, one task ahead: its latency overlaps this task's
-        // first loads (on the ticket wave, not on the polling wave)
-        uint32_t next = 0;
-        if (threadIdx.x == kTicketThread)
-            next = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int tile = run_tile_s, b = run_blk_s;
+        if (abort_s || tile < 0) return;   // workgroup-uniform
         if (res_slots && b == nblk - 1)   // the solve's last block: its residual too
             lds_block<T, FAST, 5>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi, nwc, nseg,
                                   wlo, whi, lds, 0, tile);
@@ -683,12 +791,12 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
                                   wlo, whi, lds, 0, tile);
         // publish: every wave's write-through stores drained, then one flag
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (threadIdx.x == kTicketThread) task_s[i & 1] = (int)next;
+        // the owner's next block (it claimed all of them when it started)
+        if (tile == own && threadIdx.x == 0) own_next_s = b + 1 < nblk ? b + 1 : -1;
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(flags + (size_t)tile * kPersistFlagStride, base + (unsigned)b + 1u,
+            __hip_atomic_store(lines + (size_t)tile * kPersistFlagStride, base + (unsigned)b + 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = task_s[i & 1];
     }
 }
 
@@ -818,7 +926,7 @@ void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo,
 // capped by the SGPR rule of MI355X_MICROARCH.md (Residency): at 97-112 SGPRs
 // the hardware admits 6 four-wave workgroups where the API may say 7.  Used to
 // size the tiles so one round of workgroups covers them; residency is no
-// longer a correctness condition (tickets, k_jacobi_persist).
+// longer a correctness condition (claims and stealing, k_jacobi_persist).
 template <int T, int FAST>
 int persist_blocks_per_cu(int pad) {
     static int cache[2] = {0, 0};
@@ -837,9 +945,9 @@ int persist_blocks_per_cu(int pad) {
 
 // The persistent form of launch_lds_t<T, 0> over nblk blocks: the same tile
 // geometry (pad, segments, weights), its round sized by the persistent
-// kernel's own occupancy; a grid of min(tiles, one round) workgroups takes
-// the tasks by ticket.  false (nothing launched): more tiles than
-// kPersistMaxGroups flags, or row groups shorter than two T-row bands.
+// kernel's own occupancy; one workgroup per tile.  false (nothing launched):
+// more tiles than kPersistMaxGroups lines, or row groups shorter than two
+// T-row bands.
 template <int T>
 bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
                           int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s) {
@@ -857,13 +965,11 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
     // rows for a T-row band per group: a task's input rows lie in its 3 x 3
     // neighbourhood
     if (ngrp * nwc > kPersistMaxGroups || nrows < ngrp * 2 * T) return false;
-    // CFD_PERSIST_GRID=<n>: launch n workgroups (tests: fewer than the tiles,
-    // or more than the GPU holds at once); default one round
-    // (read per launch, like the two knobs below: one getenv per solve)
+    // one workgroup per tile (each owns one); CFD_PERSIST_GRID=<n> launches
+    // n >= tiles (the surplus owns nothing and leaves).  Knobs are read per
+    // launch (one getenv each per solve) so tests can change them.
     const char *ge = getenv("CFD_PERSIST_GRID");
-    const int grid_env = ge ? std::max(1, atoi(ge)) : 0;
-    const long round = (long)g.n_cu * occ;
-    const int nwg = grid_env > 0 ? grid_env : (int)std::min<long>((long)ngrp * nwc, round);
+    const int nwg = std::max(ngrp * nwc, ge ? atoi(ge) : 0);
     const dim3 grid(nwg), block(kLdsWaves * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     constexpr int kEdgeWeight = 11;
@@ -879,10 +985,19 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
     const char *de = getenv("CFD_PERSIST_DEADLINE_US");
     const double dl_us = de ? std::max(0.0, atof(de)) : 10e6;
     const uint32_t deadline = (uint32_t)std::min(4.0e9, dl_us * 100.0);
+    // a neighbour block unclaimed after this long is stolen
+    // (CFD_PERSIST_STEAL_US, default 50 us: a block takes ~40 us at 4096^2)
+    const char *se = getenv("CFD_PERSIST_STEAL_US");
+    const double st_us = se ? std::max(0.0, atof(se)) : 50.0;
+    const uint32_t steal = (uint32_t)std::min(4.0e9, st_us * 100.0);
+    // test knob: owners of tiles w % k == 1 start 2 ms late (CFD_PERSIST_LATE=k)
+    const char *le = getenv("CFD_PERSIST_LATE");
+    const int late = le ? std::max(0, atoi(le)) : 0;
 #define CFD_LDS_PLAUNCH(FASTV)                                                                     \
     hipLaunchKernelGGL((k_jacobi_persist<T, FASTV>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
                        f.persist, f.host_nonfinite ? f.host_nonfinite + 2 : nullptr, rs, epoch, pass, \
-                       par0, nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq, deadline)
+                       par0, nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq, deadline, steal,  \
+                       late)
     if (g.fastdiv == 1)
         CFD_LDS_PLAUNCH(1);
     else if (g.fastdiv == 2)

@@ -2692,6 +2692,16 @@ int cfd_get_jacobi_geometry(const cfd_model *m, int persist, int *lds_pad, int *
     return 0;
 }
 
+int cfd_get_persist_steals(cfd_model *m, uint64_t *steals) {
+    if (!m || !steals) return fail(CFD_EINVAL, "null argument");
+    int rc = m->sync();
+    if (rc) return rc;
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, m->f.persist + 2, 4, hipMemcpyDeviceToHost));
+    *steals = v;
+    return 0;
+}
+
 int cfd_get_persist_blocks(const cfd_model *m, int *blocks) {
     if (!m || !blocks) return fail(CFD_EINVAL, "null argument");
     *blocks = m->last_persist_blocks;

@@ -241,6 +241,10 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
  * Blocks after them (shorter ones of an uneven split) are k_jacobi_lds
  * launches of their own. */
 int cfd_get_persist_blocks(const cfd_model *m, int *blocks);
+/* Blocks of persistent solves that a workgroup ran for a neighbour tile whose
+ * owner had not claimed them (k_jacobi_persist stealing; 0 when every owner
+ * was resident), summed over the model's life.  Synchronises.  (new) */
+int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
 /* The tile geometry of the model's 8-sweep kind-5 Jacobi launch over its
  * first block's rows (persist != 0: the persistent form's): the dynamic LDS
  * pad in bytes (24 KiB caps a CU at 3 four-wave workgroups on cache-resident

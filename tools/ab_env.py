@@ -1,6 +1,7 @@
 """A/B environment settings of the library on the bench workload: one fresh
 tools/tb_one.py process per (setting, round), rounds interleaved, best of
-three.  AB_CMD="parity_one.py 4096 3" (or AB_N=8192) changes the workload.
+three (AB_ROUNDS), with the median.  AB_CMD="parity_one.py 4096 3" (or AB_N=8192)
+changes the workload.
 Usage: ab_env.py "NAME=VAL[,NAME=VAL]" ...   ("" = defaults)"""
 import json
 import os
@@ -9,8 +10,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 specs = sys.argv[1:]
-best = {}
-for rnd in range(3):
+best, allv = {}, {}
+for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
     for sp in specs:
         env = dict(os.environ)
         for kv in filter(None, sp.split(",")):
@@ -27,6 +28,9 @@ for rnd in range(3):
         print(json.dumps({"setting": sp, "round": rnd, "us_per_sweep": d.get("us_per_sweep"),
                           "ms_per_step": round(d["ms_per_step"], 4),
                           "geometry": d.get("geometry"), "persist_blocks": d.get("persist_blocks"),
+                          "steals": d.get("persist_steals"),
                           "crc": d.get("state_crc32")}), flush=True)
         best[sp] = min(best.get(sp, 1e9), d[key])
-print(json.dumps({"best_" + key: best}), flush=True)
+        allv.setdefault(sp, []).append(d[key])
+med = {k: sorted(v)[len(v) // 2] for k, v in allv.items()}
+print(json.dumps({"best_" + key: best, "median_" + key: med}), flush=True)

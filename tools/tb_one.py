@@ -35,6 +35,7 @@ st = m.get_state()
 crc = zlib.crc32(b"".join(st[k].tobytes() for k in ("u", "v", "p", "p_prime")))
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("CFD_")},
                   "grid": [grid.nx, grid.ny], "geometry": m.jacobi_geometry(),
-                  "persist_blocks": m.persist_blocks, "kernel": m.kernel_config, "us_per_sweep": tm["solve_ms"] / tm["sweeps"] * 1e3,
+                  "persist_blocks": m.persist_blocks, "persist_steals": m.persist_steals,
+                  "kernel": m.kernel_config, "us_per_sweep": tm["solve_ms"] / tm["sweeps"] * 1e3,
                   "ms_per_step": tm["step_ms"] / tm["steps"], "state_crc32": crc}), flush=True)
 m.close()
