@@ -74,6 +74,8 @@ struct Ctl {
     // (0: none, it converged on its last stage); spec_launches: launches run
     // (the finalize's buffer flips).  All 0 between solves.
     int32_t spec_stop, spec_redo, spec_launch, spec_launches;
+    uint32_t spec_done;     // tickets of the running speculative launch (spec_check_tail); 0 between
+                            // launches
     int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
     uint32_t err[kMaxSweeps];        // per-sweep max |p'new - p'| as f32 bits
 };
@@ -319,6 +321,15 @@ bool correct_finish_march(const Geom &g, const Fields &f);
 void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
                            bool fold_finalize = false, const SolveFinalizeArgs *sf = nullptr);
 void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s);
+// The corrector of pass `pass` and, when pass+1 exists (has_next) and the
+// device's go flag says it runs, pass+1's head (u* <- u, v* <- v,
+// divergence) in one launch (k_correct_head4, single domain; every pass of the
+// loop uses it: the passes alternate the u* / v* arrays, and u / v are
+// written only when the loop ends); correct_head_ok: its alignment and
+// CFD_CORR_HEAD knob.
+bool correct_head_ok(const Geom &g, const Fields &f);
+void launch_correct_head(const Geom &g, const Fields &f, int pass, float dt_override, bool has_next,
+                         hipStream_t s);
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 
 // Jacobi kernel geometry (exported for the roofline bookkeeping in bench).

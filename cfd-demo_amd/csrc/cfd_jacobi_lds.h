@@ -392,7 +392,7 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           float *__restrict__ pb, const float *__restrict__ rhs,
                                           Ctl *ctl, uint32_t *res_slots, int par, int out_lo,
                                           int out_hi, int nwc, int nseg, int wlo, int whi, f2 *lds,
-                                          int nst, int bid) {
+                                          int nst, int bid, int spec_fold = 0) {
     using M = LdsMarch<T, FAST, MODE>;
     constexpr bool RES = M::RES;
     M w;
@@ -497,12 +497,23 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     else
         w.template run<0>();
     if (M::SPEC) {
+        // spec_fold: returning atomics, all of the wave's in flight at once,
+        // then one wait (the launch's last workgroup reads them: spec_check_tail)
+        unsigned acc = 0u;
 #pragma unroll
         for (int s = 0; s < T; ++s) {
             const float ms = wave_max(out_lane ? w.mm[s] : 0.0f);
-            if (lane == 0)
-                publish_max(res_slots + (size_t)s * kResSlots * kResStride, bid * kLdsWaves + wave, ms);
+            if (lane == 0 && ms > 0.0f) {
+                uint32_t *slot = res_slots + (size_t)s * kResSlots * kResStride +
+                                 ((bid * kLdsWaves + wave) & (kResSlots - 1)) * kResStride;
+                if (spec_fold)
+                    acc |= __hip_atomic_fetch_max(slot, __float_as_uint(ms), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    atomicMax(slot, __float_as_uint(ms));
+            }
         }
+        if (spec_fold) asm volatile("s_waitcnt vmcnt(0)" ::"v"(acc) : "memory");
     }
     if (!RES) return;
     const float m = wave_max(out_lane ? w.m : 0.0f);
@@ -518,11 +529,59 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
 constexpr int lds_min_waves(int mode) {
     return mode == 2 ? CFD_LDS_SPEC_WPE : (CFD_LDS_WPE > 0 ? CFD_LDS_WPE : 1);
 }
+// The speculative launch's own early-exit check (r4, replaces k_spec_check's
+// launch; CFD_SPEC_FOLD=0 keeps it): every workgroup publishes its sweeps'
+// residual maxima with RETURNING atomics and waits for them, then takes a
+// ticket (a returning device-scope add); the workgroup that draws the last
+// ticket sees every residual of the launch and folds them (atomic exchange
+// with 0: read and reset at the memory side, where the atomics were
+// performed), finds the first of the launch's sweeps below p_tol
+// (model.rs:816) and sets spec_stop / spec_launch / spec_redo for the launches
+// that follow (a kernel boundary away).  k_spec_check's logic and bits.
+inline bool spec_fold_on() {
+    const char *e = getenv("CFD_SPEC_FOLD");
+    return !(e && atoi(e) == 0);
+}
+template <int T>
+__device__ __forceinline__ void spec_check_tail(const Geom &g, Ctl *ctl, uint32_t *res_slots, int it,
+                                                int par) {
+    __shared__ int last_s;
+    __syncthreads();   // every wave's residual atomics have returned
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(&ctl->spec_done, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        last_s = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    for (int s = wv; s < T; s += kLdsWaves) {
+        uint32_t *set = res_slots + (size_t)s * kResSlots * kResStride;
+        const unsigned v = lane < kResSlots ? __hip_atomic_exchange(set + lane * kResStride, 0u,
+                                                                     __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                            : 0u;
+        const float m = fmaxf(wave_max(__uint_as_float(v)), __uint_as_float(ctl->err[it + s]));
+        if (lane == 0) ctl->err[it + s] = __float_as_uint(m);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int j = 0;
+    while (j < T && !(__uint_as_float(ctl->err[it + j]) < g.p_tol)) ++j;
+    ctl->spec_launches = par + 1;
+    if (j < T) {
+        ctl->spec_stop = 1;
+        ctl->spec_launch = par;
+        ctl->spec_redo = j + 1 < T ? j + 1 : 0;
+    }
+    ctl->spec_done = 0u;   // the next launch's tickets
+}
+
 template <int T, int FAST, int MODE>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
-    int wlo, int whi) {
+    int wlo, int whi, int it, int spec_fold) {
     using M = LdsMarch<T, FAST, MODE>;
     [[maybe_unused]] constexpr bool RES = M::RES;   // the stamp guard's
     __shared__ f2 lds[kLdsWaves * M::D * 64];
@@ -557,7 +616,8 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         par = ctl->spec_launch;   // re-run that launch: same source, same destination
     }
     lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc, nseg, wlo,
-                             whi, lds, nst, xcd_block(g));
+                             whi, lds, nst, xcd_block(g), spec_fold);
+    if (M::SPEC && spec_fold) spec_check_tail<T>(g, ctl, res_slots, it, par);
 }
 
 // Persistent fixed-count solve: ONE launch runs nblk blocks of T sweeps
@@ -870,7 +930,7 @@ int lds_segments(const Geom &g, int nrows, int nwc, int pad, int occ_override = 
 }
 
 template <int T, int MODE>
-void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
                   uint32_t *rs, hipStream_t s) {
     const int nch = g.nx / 2;
     const int nwc = cdiv(nch, LdsMarch<T, 1, MODE>::OUTL);
@@ -888,9 +948,10 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo,
     const int reach = T + 2;
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
+    const int spec_fold = MODE == 2 && spec_fold_on() ? 1 : 0;
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
     hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
-                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi)
+                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, spec_fold)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);
     else if (g.fastdiv == 2)
@@ -903,22 +964,22 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int out_lo,
 // T sweeps per launch: mode 0 / 1 (plain / last-stage residual, chosen by
 // rs != nullptr), 2 (SPEC, rs = the first stage's slot set), 3 (REDO, T = 8).
 template <int T>
-void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
                   uint32_t *rs, int mode, hipStream_t s) {
     if (mode == 2) {
-        launch_lds_t<T, 2>(g, f, pass, par, out_lo, out_hi, rs, s);
+        launch_lds_t<T, 2>(g, f, pass, par, it, out_lo, out_hi, rs, s);
         return;
     }
     if constexpr (T == 8) {
         if (mode == 3) {
-            launch_lds_t<8, 3>(g, f, pass, par, out_lo, out_hi, rs, s);
+            launch_lds_t<8, 3>(g, f, pass, par, it, out_lo, out_hi, rs, s);
             return;
         }
     }
     if (rs)
-        launch_lds_t<T, 1>(g, f, pass, par, out_lo, out_hi, rs, s);
+        launch_lds_t<T, 1>(g, f, pass, par, it, out_lo, out_hi, rs, s);
     else
-        launch_lds_t<T, 0>(g, f, pass, par, out_lo, out_hi, rs, s);
+        launch_lds_t<T, 0>(g, f, pass, par, it, out_lo, out_hi, rs, s);
 }
 
 // Workgroups of k_jacobi_persist<T, FAST> one CU holds at once with `pad`
@@ -1011,9 +1072,9 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
 }  // namespace
 
 // per-translation-unit entry points (cfd_jacobi_lds*.hip)
-void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int out_lo,
+void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int it, int out_lo,
                      int out_hi, uint32_t *rs, int mode, hipStream_t s);
-void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
                    uint32_t *rs, int mode, hipStream_t s);
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
                          int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s);

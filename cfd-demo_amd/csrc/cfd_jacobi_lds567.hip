@@ -3,14 +3,14 @@
 
 namespace cfd {
 
-void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int out_lo,
+void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int it, int out_lo,
                      int out_hi, uint32_t *rs, int mode, hipStream_t s) {
     if (T == 5)
-        launch_lds_T<5>(g, f, pass, par, out_lo, out_hi, rs, mode, s);
+        launch_lds_T<5>(g, f, pass, par, it, out_lo, out_hi, rs, mode, s);
     else if (T == 6)
-        launch_lds_T<6>(g, f, pass, par, out_lo, out_hi, rs, mode, s);
+        launch_lds_T<6>(g, f, pass, par, it, out_lo, out_hi, rs, mode, s);
     else
-        launch_lds_T<7>(g, f, pass, par, out_lo, out_hi, rs, mode, s);
+        launch_lds_T<7>(g, f, pass, par, it, out_lo, out_hi, rs, mode, s);
 }
 
 }  // namespace cfd

@@ -4,9 +4,9 @@
 
 namespace cfd {
 
-void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
                    uint32_t *rs, int mode, hipStream_t s) {
-    launch_lds_T<8>(g, f, pass, par, out_lo, out_hi, rs, mode, s);
+    launch_lds_T<8>(g, f, pass, par, it, out_lo, out_hi, rs, mode, s);
 }
 
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,

@@ -865,6 +865,154 @@ __global__ __launch_bounds__(kBlock) void k_corrector4(Geom g, Fields f, int pas
     }
 }
 
+// The corrector of pass k fused with the head of pass k+1 (model.rs:693 +
+// 698-704: apply_corrector, then u* <- u, v* <- v and rhs = div(u*, v*)/dt)
+// when the device says pass k+1 runs (Ctl::go[pass+1], set by the solve's
+// finalize before this launch); otherwise the plain corrector.  Single domain,
+// one thread per 4 cells of an allocation row.
+//
+// The corrected velocities go straight into the next pass's u* / v*, and
+// u / v get their final values only from the loop's last corrector: every
+// pass's corrector overwrites every corrected face of u and v and leaves the
+// others (u faces 0 and nx, v rows 0 and ny, ghost rows) as they are, which is
+// also what the copies give u* / v* there.  The divergence of a row needs the
+// corrected east face u(i0+4) of the next thread and v of the next row: both
+// are recomputed here from the corrector's inputs with its own expressions
+// (the same bits), so those inputs must not be overwritten by this launch --
+// the passes alternate arrays.  Pass k reads its u* / v* from u_star / v_star
+// when k is even and from u / v when k is odd, and writes the corrected values
+// to the other pair:
+//   head, k even: u_star -> u (u already holds u at the uncorrected places);
+//   head, k odd:  u -> u_star (plus u* <- u at the uncorrected places, ghost
+//                 rows included, as k_copy_star_div does);
+//   last, k even: k_corrector4 (u <- u_star - corr);
+//   last, k odd:  u_star <- u everywhere (the reference's u* of the last
+//                 pass), then u <- u - corr in place (elementwise).
+// p += p' in every pass.  32 B per cell (read u*, v*, p', p; write the other
+// pair, p, rhs) against 48 for k_corrector4 + k_copy_star_div, and one launch
+// per pass fewer.
+template <int SP>
+__device__ __forceinline__ float u_corr(const Geom &g, float us, float pr, float pw, float dt, int i) {
+    // model.rs:1336-1362; faces nx-7..nx-1 are the scalar tail: (dt * dp) / dx (Q9)
+    return i >= g.nx - 7 ? us - sdiv<SP>(dt * (pr - pw), g.dx, g.r_dx)
+                         : us - dt * sdiv<SP>(pr - pw, g.dx, g.r_dx);
+}
+
+template <int SP>
+__global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int pass,
+                                                          float dt_override, int nbx, int has_next) {
+    Ctl *c = f.ctl;
+    if (pass_off(c, pass)) return;
+    // pass+1 exists (host) and runs (device: the early exit, model.rs:721)
+    const bool head = has_next && c->go[pass + 1] != 0;
+    const bool odd = pass & 1;
+    const float *__restrict__ in_u = odd ? f.u : f.u_star;   // this pass's u*
+    const float *__restrict__ in_v = odd ? f.v : f.v_star;
+    float *__restrict__ out_u = odd ? f.u_star : f.u;        // the next pass's u*
+    float *__restrict__ out_v = odd ? f.v_star : f.v;
+    const int bid = xcd_block(g);
+    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
+    const int lr = bid / nbx - kGhostUV;   // allocation row: v rows -G..nyl+G, u rows -G..nyl+G-1
+    const int nx = g.nx, W = nx + 1, nyl = g.nyl;
+    if (i0 >= nx) return;
+    const float dt = dt_of(c, dt_override);
+    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
+    const long kc = (long)lr * nx + i0, ku = (long)lr * W + i0;
+    const bool owned = lr >= 0 && lr < nyl;
+    // u* <- u and v* <- v of the whole row (the next pass's u* at places no
+    // corrector writes, or the last odd pass's u*): only when u* is out of date
+    if (odd && (!head || !owned)) {
+        *reinterpret_cast<float4 *>(f.v_star + kc) = *reinterpret_cast<const float4 *>(f.v + kc);
+        if (lr < nyl + kGhostUV) {   // not v's extra face row
+            const float *__restrict__ ur = f.u + ku;
+            float *__restrict__ us = f.u_star + ku;
+            us[0] = ur[0];
+            us[1] = ur[1];
+            us[2] = ur[2];
+            us[3] = ur[3];
+            if (i0 + 4 == nx) us[4] = ur[4];   // face nx
+        }
+    }
+    if (!owned && (head || lr != nyl)) return;
+    auto v_row = [&](int r, const float4 &pt, bool *hit) -> float4 {
+        const int jr = g.j0 + r;
+        const long k = (long)r * nx + i0;
+        *hit = jr >= 1 && jr <= g.ny - 1;   // model.rs:1366: rows 1..ny-1
+        if (!*hit) return *reinterpret_cast<const float4 *>(f.v + k);
+        const float4 pb = *reinterpret_cast<const float4 *>(pp + k - nx);
+        const float4 vs = *reinterpret_cast<const float4 *>(in_v + k);
+        float4 o;
+        o.x = vs.x - dt * sdiv<SP>(pt.x - pb.x, g.dy, g.r_dy);
+        o.y = vs.y - dt * sdiv<SP>(pt.y - pb.y, g.dy, g.r_dy);
+        o.z = vs.z - dt * sdiv<SP>(pt.z - pb.z, g.dy, g.r_dy);
+        o.w = vs.w - dt * sdiv<SP>(pt.w - pb.w, g.dy, g.r_dy);
+        return o;
+    };
+    if (!head) {
+        // the loop's last corrector: u, v, p final (rows 0..nyl; v's row nyl)
+        float4 pc = {0.f, 0.f, 0.f, 0.f};
+        if (owned) {
+            pc = *reinterpret_cast<const float4 *>(pp + kc);
+            const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
+            const float pr[4] = {pc.x, pc.y, pc.z, pc.w};
+            const float pw[4] = {pl, pc.x, pc.y, pc.z};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = i0 + q;
+                if (i < 1 || i > nx - 1) continue;
+                f.u[ku + q] = u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i);
+            }
+        }
+        bool hit;
+        const float4 o = v_row(lr, owned ? pc : *reinterpret_cast<const float4 *>(pp + kc), &hit);
+        if (hit) *reinterpret_cast<float4 *>(f.v + kc) = o;
+        if (owned) {
+            float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
+            pv.x = pv.x + pc.x;
+            pv.y = pv.y + pc.y;
+            pv.z = pv.z + pc.z;
+            pv.w = pv.w + pc.w;
+            *reinterpret_cast<float4 *>(f.p + kc) = pv;
+        }
+        return;
+    }
+    // ---- an owned row: corrector k, then pass k+1's copy and divergence
+    const float4 pc = *reinterpret_cast<const float4 *>(pp + kc);
+    const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
+    const float p4 = i0 + 4 < nx ? pp[kc + 4] : 0.0f;   // for the east face i0+4
+    const float pr[5] = {pc.x, pc.y, pc.z, pc.w, p4};
+    const float pw[5] = {pl, pc.x, pc.y, pc.z, pc.w};
+    float un[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const int i = i0 + q;
+        un[q] = (i >= 1 && i <= nx - 1) ? u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i)
+                                        : f.u[ku + q];   // faces 0 and nx keep u
+    }
+    out_u[ku] = un[0];
+    out_u[ku + 1] = un[1];
+    out_u[ku + 2] = un[2];
+    out_u[ku + 3] = un[3];
+    if (i0 + 4 == nx) out_u[ku + 4] = un[4];
+    bool hit;
+    const float4 vlo = v_row(lr, pc, &hit);
+    const float4 vhi = v_row(lr + 1, *reinterpret_cast<const float4 *>(pp + kc + nx), &hit);
+    *reinterpret_cast<float4 *>(out_v + kc) = vlo;
+    float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
+    pv.x = pv.x + pc.x;
+    pv.y = pv.y + pc.y;
+    pv.z = pv.z + pc.z;
+    pv.w = pv.w + pc.w;
+    *reinterpret_cast<float4 *>(f.p + kc) = pv;
+    const float rdx = g.r_dx, rdy = g.r_dy, dx = g.dx, dy = g.dy;
+    float4 r;   // k_divergence's expression on the new u*, v*
+    r.x = (sdiv<SP>(un[1] - un[0], dx, rdx) + sdiv<SP>(vhi.x - vlo.x, dy, rdy)) / dt;
+    r.y = (sdiv<SP>(un[2] - un[1], dx, rdx) + sdiv<SP>(vhi.y - vlo.y, dy, rdy)) / dt;
+    r.z = (sdiv<SP>(un[3] - un[2], dx, rdx) + sdiv<SP>(vhi.z - vlo.z, dy, rdy)) / dt;
+    r.w = (sdiv<SP>(un[4] - un[3], dx, rdx) + sdiv<SP>(vhi.w - vlo.w, dy, rdy)) / dt;
+    *reinterpret_cast<float4 *>(f.rhs + kc) = r;
+}
+
 // ------------------------------------------------- velocity boundaries (K6)
 
 // Inlet face value of row j (model.rs:830-846): uniform or parabolic, >= 0.
@@ -1587,6 +1735,24 @@ void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_overrid
     else
         hipLaunchKernelGGL(k_corrector<0>, dim3(nbx * (g.nyl + 1)), dim3(kBlock), 0, s, g, f, pass,
                            dt_override, nbx);
+}
+
+bool correct_head_ok(const Geom &g, const Fields &f) {
+    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+    const char *e = getenv("CFD_CORR_HEAD");   // 0: corrector + separate pass head
+    return !(e && atoi(e) == 0) && g.nx % 4 == 0 && a16(f.v) && a16(f.v_star) && a16(f.p) &&
+           a16(f.pp[0]) && a16(f.pp[1]) && a16(f.rhs);
+}
+
+void launch_correct_head(const Geom &g, const Fields &f, int pass, float dt_override, bool has_next,
+                         hipStream_t s) {
+    const int nbx4 = cdiv(g.nx / 4, kBlock);
+    const dim3 grid(nbx4 * (g.nyl + 1 + 2 * kGhostUV));
+    const int hn = has_next ? 1 : 0;
+    if (g.sp_pow2)
+        hipLaunchKernelGGL(k_correct_head4<1>, grid, dim3(kBlock), 0, s, g, f, pass, dt_override, nbx4, hn);
+    else
+        hipLaunchKernelGGL(k_correct_head4<0>, grid, dim3(kBlock), 0, s, g, f, pass, dt_override, nbx4, hn);
 }
 
 bool correct_finish_folds_finalize(const Geom &g, const Fields &f) {

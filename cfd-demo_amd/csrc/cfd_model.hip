@@ -1117,7 +1117,9 @@ struct cfd_model {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
                     launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream);
-                    launch_spec_check(g, f, pass, it, T, launches, stream);
+                    // the launch's last workgroup checks (spec_check_tail) unless
+                    // CFD_SPEC_FOLD=0 (then a one-workgroup launch after it)
+                    if (!spec_fold_env) launch_spec_check(g, f, pass, it, T, launches, stream);
                     it += T;
                     ++launches;
                 }
@@ -1421,6 +1423,10 @@ struct cfd_model {
         const char *e = getenv("CFD_SPEC");
         return !(e && atoi(e) == 0);
     }();
+    bool spec_fold_env = [] {
+        const char *e = getenv("CFD_SPEC_FOLD");
+        return !(e && atoi(e) == 0);
+    }();
     bool spec_mode() const {
         return spec_env && !sharded() && g.tol_enabled &&
                params.pressure_solver == CFD_SOLVER_JACOBI;
@@ -1495,12 +1501,24 @@ struct cfd_model {
             first_divergence(0);
             int rc = enqueue_solve(0);
             if (rc) return rc;
-            launch_corrector(g, f, 0, dt_override, stream);
-            for (int pass = 1; pass <= params.corrector_passes; ++pass) {
-                pass_head(pass, dt_override);
+            // single domain: each corrector that a further pass follows also
+            // does that pass's head, as the device's go flag decides
+            // (k_correct_head4; every pass, the last included, runs it: the
+            // passes alternate the u* / v* arrays)
+            const int passes = params.corrector_passes;
+            const bool fuse = !sharded() && passes >= 1 && correct_head_ok(g, f);
+            auto corrector = [&](int pass) {
+                if (fuse)
+                    launch_correct_head(g, f, pass, dt_override, pass < passes, stream);
+                else
+                    launch_corrector(g, f, pass, dt_override, stream);
+            };
+            corrector(0);
+            for (int pass = 1; pass <= passes; ++pass) {
+                if (!fuse) pass_head(pass, dt_override);
                 rc = enqueue_solve(pass);
                 if (rc) return rc;
-                launch_corrector(g, f, pass, dt_override, stream);
+                corrector(pass);
             }
         } else {
             first_divergence(-1);

@@ -376,3 +376,39 @@ def test_kernel_selection_rules(monkeypatch):
     m = c.Model(c.cavity_grid(1024), p)
     assert m.kernel_config == {"fastdiv": 0, "temporal": 4} and m.jacobi_kernel["kind"] == 4
     m.close()
+
+
+@pytest.mark.parametrize("passes,tol", [(1, False), (2, False), (3, False), (20, True)])
+def test_corrector_head_fused_matches_separate(monkeypatch, passes, tol):
+    """k_correct_head4 (r4): the corrector of pass k with pass k+1's copy and
+    divergence in one launch, the passes alternating the u* / v* arrays, u / v
+    written only by the loop's last corrector.  Bitwise against the separate
+    launches (CFD_CORR_HEAD=0) in every field the step leaves -- u* and v*
+    included -- with the loop ending on odd and even passes, fixed (1-3
+    passes) and by the reference's early exit (20 passes, tolerance on), on
+    the cavity and on the channel with the cylinder, and against the oracle."""
+    c = _cfd()
+    cases = [
+        (dict(nx=256, ny=128, lx=2.0, ly=1.0, cylinder=None),
+         dict(bc_kind=1, viscosity=0.001, jacobi_iters=23, corrector_passes=passes, tol_enabled=tol)),
+        (dict(nx=800, ny=264, lx=30.0, ly=10.0, cylinder=(7.5, 5.0, 0.75)),
+         dict(jacobi_iters=30, corrector_passes=passes, tol_enabled=tol, scheme=1)),
+    ]
+    fields = ("u", "v", "p", "p_prime", "u_star", "v_star", "rhs")
+    for g, kw in cases:
+        got = {}
+        for env in ("0", "1"):
+            monkeypatch.setenv("CFD_CORR_HEAD", env)
+            m = c.Model(_grid(g), _params(kw))
+            for _ in range(6):
+                m.update()
+            got[env] = m.get_state()
+            m.close()
+        o = _oracle(g, **kw)
+        for _ in range(6):
+            o.update()
+        for f in fields:
+            assert_bitwise(f"{g['nx']}x{g['ny']} passes={passes} fused vs separate:{f}", got["1"][f],
+                           got["0"][f])
+            assert_bitwise(f"{g['nx']}x{g['ny']} passes={passes} fused vs oracle:{f}", got["1"][f],
+                           o.field(f))
