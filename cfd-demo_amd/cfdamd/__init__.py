@@ -449,6 +449,14 @@ class Model:
         return int(n.value)
 
     @property
+    def persist_sums(self) -> int:
+        """Persistent-solve blocks run in the guarded SUMS form
+        (cfd_get_persist_sums)."""
+        n = C.c_uint64()
+        check("cfd_get_persist_sums", load().cfd_get_persist_sums(self._hh(), C.byref(n)))
+        return int(n.value)
+
+    @property
     def persist_blocks(self) -> int:
         """8-sweep blocks the last fixed-count solve ran in one persistent
         launch (k_jacobi_persist); 0 when every block had its own launch."""

@@ -36,8 +36,10 @@ constexpr int kMaxPasses = 64;     // corrector passes + 1
 constexpr int kResSlots = 32;
 constexpr int kResStride = 16;
 // persistent-solve words (k_jacobi_persist), one 64-B line each: line 0 [1]
-// the abort flag, [2] the blocks stolen so far; then one line per tile: [0]
-// its done flag, [1] its claim counter
+// the abort flag, [2] the blocks stolen so far, [3] the blocks run in the
+// SUMS form so far; then one line per tile: [0] its done flag, [1] its claim
+// counter, [2..5] / [6..9] its waves' max |p'| stored in its last even / odd
+// block
 constexpr int kPersistFlagStride = 16;
 constexpr int kPersistHeadLines = 1;
 // flag = epoch << kPersistBlockBits | blocks done: room for every block of the

@@ -28,6 +28,8 @@
 // packed back into a v_pk_add_f32 (VOP3P cannot take DPP); the rest of the
 // update is explicit packed f32 arithmetic on column pairs.
 #pragma once
+#include <cmath>
+
 #include "cfd_device.h"
 
 namespace cfd {
@@ -105,7 +107,16 @@ constexpr int ring_depth(int T, int PD, int G) {
 // once an earlier launch of the solve converged (Ctl::spec_stop); 3 (REDO)
 // re-runs the converged launch from its untouched source buffer with the
 // run-time stage count Ctl::spec_redo < T (stores only the segment's rows).
-template <int T, int FAST, int MODE>
+// SUMS (persistent launches only, FAST == 1 with dx^2 == dy^2 a power of two,
+// r4): the update forms (h + v) * (1/dx^2) instead of h * (1/dx^2) +
+// v * (1/dy^2) -- one packed multiply per column pair and stage fewer (10
+// VALU instructions instead of 11).  Bitwise the same whenever |h|, |v| <
+// 2^104: both products are then exact scalings by a power of two, and
+// RN(R h + R v) = R RN(h + v) for R = 2^k (scaling commutes with rounding,
+// overflow included; a subnormal h + v is exact).  k_jacobi_persist proves
+// that bound per task before it picks SUMS (its guard); otherwise, and for
+// every other launch, the reference's form runs.
+template <int T, int FAST, int MODE, bool SUMS = false>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1 || MODE == 5, SPEC = MODE == 2, REDO = MODE == 3;
     // MODE 4 (PERSIST): a block of k_jacobi_persist; p' moves between
@@ -113,6 +124,15 @@ struct LdsMarch {
     // write through (sc1 both ways, MI355X_MICROARCH.md visibility rules).
     // MODE 5: its last block, which also publishes the residual (RES)
     static constexpr bool PERSIST = MODE == 4 || MODE == 5;
+    // persistent blocks in the reference's form track what the SUMS guard
+    // needs: max |p'| of the rows the wave loads (imax) and of the rhs rows it
+    // uses (rmax); every persistent block tracks max |p'| of the rows it
+    // stores (omax), which are its neighbours' inputs in the next block
+#ifndef CFD_PROBE_NOTRACK
+#define CFD_PROBE_NOTRACK 0   // (diagnostic builds: no guard tracking)
+#endif
+    static constexpr bool TRACK_IN = PERSIST && !SUMS && !CFD_PROBE_NOTRACK;
+    static_assert(!SUMS || (FAST == 1 && PERSIST), "SUMS: persistent, reciprocal multiply");
     static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
     static constexpr int PST_AUX = PERSIST ? 16 : CFD_LDS_ST_AUX;
     // Stage s of slot v computes row k - s - off(s).  With G = 1 (off = 0)
@@ -156,6 +176,7 @@ struct LdsMarch {
     float dx_sq, r_dx_sq, dy_sq, r_dy_sq, denom, r_denom;
     __amdgpu_buffer_rsrc_t rs_p, rs_r, rs_d;
     float m;
+    float omax, imax, rmax;   // PERSIST: the guard's maxima (above)
     float mm[SPEC ? T : 1];   // SPEC: stage s's residual (segment rows only)
     int r0v, r1v;             // the segment's output rows (march order)
     int nst;                  // REDO: stages to run (< T)
@@ -188,9 +209,15 @@ struct LdsMarch {
         const float hy = C.x + from_right(C.x);
         const f2 h = {hx, hy};
         const f2 v = Tp + B;
-        const f2 hz = fdiv2<FAST>(h, dx_sq, r_dx_sq);
-        const f2 vt = fdiv2<FAST>(v, dy_sq, r_dy_sq);
-        const f2 pu = fdiv2<FAST>(hz + vt - Rh, denom, r_denom);
+        f2 s;
+        if constexpr (SUMS) {
+            s = (h + v) * r_dx_sq;   // == h * r_dx_sq + v * r_dy_sq under the guard
+        } else {
+            const f2 hz = fdiv2<FAST>(h, dx_sq, r_dx_sq);
+            const f2 vt = fdiv2<FAST>(v, dy_sq, r_dy_sq);
+            s = hz + vt;
+        }
+        const f2 pu = fdiv2<FAST>(s - Rh, denom, r_denom);
         const float omega = 0.75f;
         const float om1 = 1.0f - omega;
         return omega * pu + om1 * C;
@@ -250,6 +277,13 @@ struct LdsMarch {
             const f2 &C = W[s - 1][(V_ - dl - 1 + kW) % NW];         //            row r
             const f2 &Tp = W[s - 1][(V_ - dl + kW) % NW];            //            row r+1
             if (REDO && s > nst) continue;                            // wave-uniform
+            if constexpr (TRACK_IN) {
+                // stage 1 reads every input row (as Tp, once) and every rhs row
+                if (s == 1) {
+                    imax = fmaxf(fmaxf(imax, fabsf(Tp.x)), fabsf(Tp.y));
+                    rmax = fmaxf(fmaxf(rmax, fabsf(rh.x)), fabsf(rh.y));
+                }
+            }
             f2 n = stage<E>(B, C, Tp, rh);
             if constexpr (SPEC) {
                 // every stage is one reference sweep: its max |new - old|.
@@ -306,6 +340,11 @@ struct LdsMarch {
                 st(n, ra);
                 if ((E & kRow) && r == g_first) st(n, g_zero);
                 if ((E & kRow) && r == g_last) st(n, g_top);
+#ifndef CFD_PROBE_NOOMAX
+#define CFD_PROBE_NOOMAX 0
+#endif
+                if constexpr (PERSIST && !CFD_PROBE_NOTRACK && !CFD_PROBE_NOOMAX)
+                    omax = fmaxf(fmaxf(omax, fabsf(n.x)), fabsf(n.y));
             }
         }
     }
@@ -387,18 +426,23 @@ struct LdsMarch {
 // k_jacobi_lds; k_jacobi_persist runs it once per block).  `bid`: the
 // workgroup's (XCD-renumbered) index.  Returns without touching memory for
 // waves with no rows.
-template <int T, int FAST, int MODE>
+// trk (persistent blocks): per wave, trk[3 w .. 3 w + 2] = max |p'| of the
+// rows it stored, of the p' rows it loaded and of the rhs rows it used (the
+// last two only in the reference's form; 0 where not tracked or no rows).
+template <int T, int FAST, int MODE, bool SUMS = false>
 __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           float *__restrict__ pb, const float *__restrict__ rhs,
                                           Ctl *ctl, uint32_t *res_slots, int par, int out_lo,
                                           int out_hi, int nwc, int nseg, int wlo, int whi, f2 *lds,
-                                          int nst, int bid, int spec_fold = 0) {
-    using M = LdsMarch<T, FAST, MODE>;
+                                          int nst, int bid, int spec_fold = 0,
+                                          float *trk = nullptr) {
+    using M = LdsMarch<T, FAST, MODE, SUMS>;
     constexpr bool RES = M::RES;
     M w;
     w.nst = nst;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int lane = (int)threadIdx.x & 63;
+    if (M::PERSIST && trk && lane == 0) trk[3 * wave] = trk[3 * wave + 1] = trk[3 * wave + 2] = 0.0f;
     const int wc = bid % nwc;
     const int seg = (bid / nwc) * kLdsWaves + wave;
     const int nrows = out_hi - out_lo;
@@ -456,6 +500,7 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     w.g_top = g.ny - 1 - g.j0;
     w.g_zero = -g.j0;
     w.m = 0.0f;
+    w.omax = w.imax = w.rmax = 0.0f;
 #pragma unroll
     for (int s = 0; s < (M::SPEC ? T : 1); ++s) w.mm[s] = 0.0f;
     w.r0v = r0;
@@ -496,6 +541,16 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         w.template run<M::kCol>();
     else
         w.template run<0>();
+    if (M::PERSIST && trk) {
+        const float o = wave_max(out_lane ? w.omax : 0.0f);
+        const float im = M::TRACK_IN ? wave_max(w.imax) : 0.0f;
+        const float rm = M::TRACK_IN ? wave_max(w.rmax) : 0.0f;
+        if (lane == 0) {
+            trk[3 * wave] = o;
+            trk[3 * wave + 1] = im;
+            trk[3 * wave + 2] = rm;
+        }
+    }
     if (M::SPEC) {
         // spec_fold: returning atomics, all of the wave's in flight at once,
         // then one wait (the launch's last workgroup reads them: spec_check_tail)
@@ -671,20 +726,41 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 // sets the abort word persist[1], every workgroup leaves at its next poll or
 // at entry, and a zero-copy host word makes the model's next cfd_* call report
 // CFD_ETIMEOUT (a fault: residency no longer causes one).
+//
+// SUMS guard (r4; sums != 0 when the grid allows the form at all, LdsMarch):
+// task (t, b) of the owner runs the SUMS form when every p' value it reads is
+// below plim = 2^124 / R and every rhs value below rlim = 2^124, which keeps
+// every value its 8 sweeps form below 2^126 / R (a sweep adds at most
+// 0.1875 |rhs| / R to max |p'|: |hz + vt| <= 4 R max|p'| = denom max|p'|), so
+// R |h|, R |v| < 2^127.  What a task reads: rows its 3 x 3 neighbours stored in
+// block b-1 -- each wave publishes max |p'| of its stores with the tile's
+// flag, in the tile's line (words 2-5 / 6-9 by block parity) -- and rows no
+// tile of this launch writes (a slab's rows beyond its band), constant during
+// the launch but different in the two p' buffers: blocks 0 and 1 run the
+// reference's form and measure the tile's inputs in each buffer (and its rhs
+// rows); a stolen task runs the reference's form.  max is NaN-ignoring: a NaN
+// propagates through either form as the same operand.
 constexpr int kStealDepth = 16;
+#ifndef CFD_PERSIST_WPE
+#define CFD_PERSIST_WPE 3   // the padded launch's 3 waves per SIMD: at most 168 VGPRs
+#endif
 template <int T, int FAST>
-__global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_persist(
+__global__ __launch_bounds__(kLdsWaves * 64, CFD_PERSIST_WPE) void k_jacobi_persist(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *persist, uint32_t *host_fail, uint32_t *res_slots, uint32_t epoch, int pass,
     int par0, int nblk, int out_lo, int out_hi, int nwc, int nseg, int wlo, int whi, int ngrp,
-    int acq, uint32_t deadline, uint32_t steal, int late) {
+    int acq, uint32_t deadline, uint32_t steal, int late, int sums, float plim, float rlim) {
     using M = LdsMarch<T, FAST, 4>;
     __shared__ f2 lds[kLdsWaves * M::D * 64];
     // control (wave 0 writes, everyone reads after a barrier): the task to
     // run, the claimed-task stack, the owner's next claimed block
     // (-2: claim it now, -1: none left)
-    __shared__ int run_tile_s, run_blk_s, abort_s, own_next_s, sp_s;
+    __shared__ int run_tile_s, run_blk_s, abort_s, own_next_s, sp_s, fast_s;
     __shared__ int stk_tile[kStealDepth], stk_blk[kStealDepth];
+    // the SUMS guard: per-wave maxima of the block just run (lds_block trk),
+    // the own tile's input maxima per p' buffer and its rhs maximum
+    __shared__ float trk_s[3 * kLdsWaves], own_im_s[2], own_rm_s;
+    __shared__ int own_ok_s[2], nfast_s;
     if (pass_off(ctl, pass)) return;
     const int ntiles = ngrp * nwc;
     const int own = xcd_block(g);
@@ -720,6 +796,9 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
     if (threadIdx.x == 0) {
         sp_s = 0;
         own_next_s = -2;
+        own_ok_s[0] = own_ok_s[1] = 0;
+        own_im_s[0] = own_im_s[1] = own_rm_s = 0.0f;
+        nfast_s = 0;
         // fail fast after an abort (every later launch of the model too)
         abort_s = __hip_atomic_load(persist + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         if (late > 0 && own % late == 1) {   // test knob: this owner starts late (not resident)
@@ -733,7 +812,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
         if (threadIdx.x < 64) {
             // ---- wave 0: the next task that is ready (claiming / stealing) ----
             int sp = sp_s, run_t = -1, run_b = -1;
-            bool fail = false;
+            bool fail = false, fast = false;
             if (sp == 0) {
                 int nb = own_next_s;
                 if (nb == -2) {
@@ -825,6 +904,19 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
                     } else {
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps loads below the poll
                     }
+                    if (sums && tt == own && bb >= 2 && own_ok_s[bb & 1] && own_rm_s < rlim &&
+                        own_im_s[bb & 1] < plim) {
+                        // the neighbours' stores of block bb-1 (published with their flags)
+                        float mo = 0.0f;
+                        if (nbr) {
+                            const uint32_t *q = w + 2 + 4 * ((bb - 1) & 1);
+#pragma unroll
+                            for (int k = 0; k < kLdsWaves; ++k)
+                                mo = fmaxf(mo, __uint_as_float(__hip_atomic_load(
+                                                   q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+                        }
+                        fast = wave_max(mo) < plim;
+                    }
                     break;
                 }
             }
@@ -832,6 +924,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
                 sp_s = sp;
                 run_tile_s = run_t;
                 run_blk_s = run_b;
+                fast_s = fast;
                 abort_s = fail;
                 if (fail) {
                     __hip_atomic_store(persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -842,21 +935,67 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(0)) void k_jacobi_per
         }
         __syncthreads();
         const int tile = run_tile_s, b = run_blk_s;
-        if (abort_s || tile < 0) return;   // workgroup-uniform
-        if (res_slots && b == nblk - 1)   // the solve's last block: its residual too
-            lds_block<T, FAST, 5>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi, nwc, nseg,
-                                  wlo, whi, lds, 0, tile);
-        else
-            lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc, nseg,
-                                  wlo, whi, lds, 0, tile);
+        if (abort_s || tile < 0) {   // workgroup-uniform
+            if (threadIdx.x == 0 && nfast_s)   // diagnostics: blocks run in the SUMS form
+                __hip_atomic_fetch_add(persist + 3, (uint32_t)nfast_s, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        const bool fast = fast_s;
+        const bool res = res_slots && b == nblk - 1;   // the solve's last block: its residual too
+#ifndef CFD_PROBE_NOSUMS
+#define CFD_PROBE_NOSUMS 0   // (diagnostic builds: the reference's form only)
+#endif
+        if constexpr (FAST == 1 && !CFD_PROBE_NOSUMS) {
+            if (fast) {
+                if (res)
+                    lds_block<T, FAST, 5, true>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi,
+                                                nwc, nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+                else
+                    lds_block<T, FAST, 4, true>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi,
+                                                nwc, nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+            }
+        }
+        if (!fast) {
+            if (res)
+                lds_block<T, FAST, 5>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi, nwc,
+                                      nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+            else
+                lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc,
+                                      nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+        }
+        // every wave's max |p'| stored, with (before) the flag: the next
+        // block's guard of the neighbours (written through, drained below)
+        if (sums && lane == 0) {
+            const int wv = (int)threadIdx.x >> 6;
+            __hip_atomic_store(lines + (size_t)tile * kPersistFlagStride + 2 + 4 * (b & 1) + wv,
+                               __float_as_uint(trk_s[3 * wv]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // publish: every wave's write-through stores drained, then one flag
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // the owner's next block (it claimed all of them when it started)
-        if (tile == own && threadIdx.x == 0) own_next_s = b + 1 < nblk ? b + 1 : -1;
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
+            // the owner's next block (it claimed all of them when it started)
+            if (tile == own) {
+                own_next_s = b + 1 < nblk ? b + 1 : -1;
+                if (fast) {
+                    ++nfast_s;
+                } else {
+                    // the tile's inputs in the buffer block b read, and its rhs
+                    float im = 0.0f, rm = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < kLdsWaves; ++k) {
+                        im = fmaxf(im, trk_s[3 * k + 1]);
+                        rm = fmaxf(rm, trk_s[3 * k + 2]);
+                    }
+                    own_im_s[b & 1] = fmaxf(own_im_s[b & 1], im);
+                    own_ok_s[b & 1] = 1;
+                    own_rm_s = fmaxf(own_rm_s, rm);
+                }
+            }
             __hip_atomic_store(lines + (size_t)tile * kPersistFlagStride, base + (unsigned)b + 1u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1054,11 +1193,21 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
     // test knob: owners of tiles w % k == 1 start 2 ms late (CFD_PERSIST_LATE=k)
     const char *le = getenv("CFD_PERSIST_LATE");
     const int late = le ? std::max(0, atoi(le)) : 0;
+    // the SUMS form (LdsMarch): reciprocal multiply, dx^2 == dy^2 with a
+    // power-of-two reciprocal R >= 1 (h * R, v * R exact below overflow);
+    // CFD_JACOBI_SUMS=0 keeps the reference's form everywhere
+    const char *ue = getenv("CFD_JACOBI_SUMS");
+    int exp2 = 0;
+    const float R = g.r_dx_sq;
+    const bool pow2 = R >= 1.0f && std::frexp(R, &exp2) == 0.5f;
+    const int sums = !(ue && atoi(ue) == 0) && g.fastdiv == 1 && g.dx_sq == g.dy_sq &&
+                     g.r_dx_sq == g.r_dy_sq && pow2;
+    const float plim = sums ? std::ldexp(1.0f, 124) / R : 0.0f, rlim = std::ldexp(1.0f, 124);
 #define CFD_LDS_PLAUNCH(FASTV)                                                                     \
     hipLaunchKernelGGL((k_jacobi_persist<T, FASTV>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
                        f.persist, f.host_nonfinite ? f.host_nonfinite + 2 : nullptr, rs, epoch, pass, \
                        par0, nblk, out_lo, out_hi, nwc, nseg, wlo, whi, ngrp, acq, deadline, steal,  \
-                       late)
+                       late, sums, plim, rlim)
     if (g.fastdiv == 1)
         CFD_LDS_PLAUNCH(1);
     else if (g.fastdiv == 2)

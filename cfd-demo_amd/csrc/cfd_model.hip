@@ -2720,6 +2720,16 @@ int cfd_get_persist_steals(cfd_model *m, uint64_t *steals) {
     return 0;
 }
 
+int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks) {
+    if (!m || !blocks) return fail(CFD_EINVAL, "null argument");
+    int rc = m->sync();
+    if (rc) return rc;
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, m->f.persist + 3, 4, hipMemcpyDeviceToHost));
+    *blocks = v;
+    return 0;
+}
+
 int cfd_get_persist_blocks(const cfd_model *m, int *blocks) {
     if (!m || !blocks) return fail(CFD_EINVAL, "null argument");
     *blocks = m->last_persist_blocks;

@@ -245,6 +245,11 @@ int cfd_get_persist_blocks(const cfd_model *m, int *blocks);
  * owner had not claimed them (k_jacobi_persist stealing; 0 when every owner
  * was resident), summed over the model's life.  Synchronises.  (new) */
 int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
+/* Persistent-solve blocks (per tile) run in the SUMS form -- (h + v) / dx^2
+ * for h / dx^2 + v / dy^2, one instruction per column pair and sweep fewer,
+ * taken only where a per-task guard proves it bitwise (k_jacobi_persist) --
+ * summed over the model's life.  Synchronises.  (new; diagnostics) */
+int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
 /* The tile geometry of the model's 8-sweep kind-5 Jacobi launch over its
  * first block's rows (persist != 0: the persistent form's): the dynamic LDS
  * pad in bytes (24 KiB caps a CU at 3 four-wave workgroups on cache-resident

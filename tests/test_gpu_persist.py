@@ -335,3 +335,51 @@ def test_kind5_fields_over_1GiB(monkeypatch):
     for f in ("u", "v", "p_prime", "rhs"):
         assert_bitwise(f"kind5 >1GiB:{f}", states[1][f], states[0][f])
     assert np.count_nonzero(states[1]["p_prime"]) > 0
+
+
+def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
+    """The SUMS form ((h + v) / dx^2 for h / dx^2 + v / dy^2, bitwise while
+    every value stays far below overflow) runs on a power-of-two square grid,
+    and the per-task guard falls back to the reference's form where a task
+    reads a huge value: p' = 2^110 in one corner (the tiles there and those
+    its values reach), rhs = 2^126 (> the 2^124 limit) in one patch (the
+    tiles that read it); distant tiles keep SUMS.  Every case bitwise vs
+    per-launch solves (CFD_PERSIST=0) and vs CFD_JACOBI_SUMS=0."""
+    import cfdamd
+    grid = cfdamd.cavity_grid(1024)
+    params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
+    m = cfdamd.Model(grid, params, device=0)
+    try:
+        m.update_n(20)
+        base = m.get_state()
+    finally:
+        m.close()
+    n = grid.nx
+    pp_huge = base["p_prime"].copy().reshape(-1, n)
+    pp_huge[5:40, 5:60] = np.float32(2.0 ** 110)
+    rhs_huge = base["rhs"].copy().reshape(-1, n)
+    rhs_huge[500:520, 300:340] = np.float32(2.0 ** 126)
+    cases = {"plain": {}, "huge_pp": {"p_prime": pp_huge.ravel()},
+             "huge_rhs": {"rhs": rhs_huge.ravel()}}
+    envs = {"per_launch": {"CFD_PERSIST": "0"}, "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0"},
+            "sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "1"}}
+    sums = {}
+    for name, inject in cases.items():
+        out = {}
+        for key, env in envs.items():
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            mm = cfdamd.Model(grid, params, device=0)
+            try:
+                mm.set_state(**dict(base, **inject))
+                mm.jacobi_pressure()
+                out[key] = (mm.get_state()["p_prime"], mm.persist_blocks, mm.persist_sums)
+            finally:
+                mm.close()
+        for key, (pp, _, _) in out.items():
+            assert_bitwise(f"sums {name} [{key}]:p_prime", pp, out["per_launch"][0])
+        assert out["sums"][1] == 25 and out["no_sums"][2] == 0, (out["sums"][1:], out["no_sums"][1:])
+        sums[name] = out["sums"][2]
+    # plain: the owned tiles' blocks 2..24 (blocks 0 and 1 measure the inputs)
+    assert sums["plain"] > 0, sums
+    assert 0 < sums["huge_pp"] < sums["plain"] and 0 < sums["huge_rhs"] < sums["plain"], sums
