@@ -404,9 +404,9 @@ def roofline_entry(model, nx, nyl, launch_ms, bench_kernel_note=None):
     cells = nx * nyl
     one_pass = BYTES_PER_CELL_UPDATE * cells
     achieved = one_pass / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(kname, f"{nx}x{nyl}")
+    traffic, traffic_src, pmc_blocks = pmc_traffic(kname, f"{nx}x{nyl}")
     if traffic:
-        traffic /= nblk   # per 8-sweep block
+        traffic /= pmc_blocks or nblk   # per 8-sweep block of the profiled dispatch
     meas = traffic / (launch_ms * 1e-3) / 1e9 if traffic and launch_ms > 0 else None
     return {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -449,6 +449,7 @@ def roofline_valu(kernel, slab, launch_ms, blocks=1):
             continue
         k = d.get("kernels", {}).get(kernel)
         if k and d.get("workload") == slab and k.get("SQ_INSTS_VALU") and launch_ms > 0:
+            blocks = k.get("blocks_per_dispatch") or blocks   # the profiled run's own count
             rate = k["SQ_INSTS_VALU"] / blocks / (launch_ms * 1e-3)
             return {"bound": "valu", "achieved": rate / 1e9, "peak": VALU_ISSUE_PEAK / 1e9,
                     "unit": "G wave64-VALU-instructions/s", "frac": rate / VALU_ISSUE_PEAK,
@@ -473,8 +474,8 @@ def pmc_traffic(kernel, slab):
             continue
         k = d.get("kernels", {}).get(kernel)
         if k and d.get("workload") == slab:
-            return k["traffic_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+            return k["traffic_bytes"], os.path.relpath(path, ROOT), k.get("blocks_per_dispatch")
+    return None, None, None
 
 
 def control_run(args, cfdamd, device, n=8192, steps=10):

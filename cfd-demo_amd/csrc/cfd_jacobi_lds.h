@@ -585,7 +585,10 @@ constexpr int lds_min_waves(int mode) {
     return mode == 2 ? CFD_LDS_SPEC_WPE : (CFD_LDS_WPE > 0 ? CFD_LDS_WPE : 1);
 }
 // The speculative launch's own early-exit check (r4, replaces k_spec_check's
-// launch; CFD_SPEC_FOLD=0 keeps it): every workgroup publishes its sweeps'
+// launch; opt-in with CFD_SPEC_FOLD=1 -- on MI355X the device-scope ticket and
+// the returning atomics cost more than the one-workgroup launch they save:
+// C3 parity mode 11.28 vs 10.83 ms/step, profiles/r4/ab_parity_r4g.log):
+// every workgroup publishes its sweeps'
 // residual maxima with RETURNING atomics and waits for them, then takes a
 // ticket (a returning device-scope add); the workgroup that draws the last
 // ticket sees every residual of the launch and folds them (atomic exchange
@@ -595,7 +598,7 @@ constexpr int lds_min_waves(int mode) {
 // that follow (a kernel boundary away).  k_spec_check's logic and bits.
 inline bool spec_fold_on() {
     const char *e = getenv("CFD_SPEC_FOLD");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) != 0;
 }
 template <int T>
 __device__ __forceinline__ void spec_check_tail(const Geom &g, Ctl *ctl, uint32_t *res_slots, int it,

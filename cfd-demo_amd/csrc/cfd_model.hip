@@ -1118,7 +1118,7 @@ struct cfd_model {
                     plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
                     launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream);
                     // the launch's last workgroup checks (spec_check_tail) unless
-                    // CFD_SPEC_FOLD=0 (then a one-workgroup launch after it)
+                    // CFD_SPEC_FOLD=1; by default a one-workgroup launch after it
                     if (!spec_fold_env) launch_spec_check(g, f, pass, it, T, launches, stream);
                     it += T;
                     ++launches;
@@ -1425,7 +1425,7 @@ struct cfd_model {
     }();
     bool spec_fold_env = [] {
         const char *e = getenv("CFD_SPEC_FOLD");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     bool spec_mode() const {
         return spec_env && !sharded() && g.tol_enabled &&

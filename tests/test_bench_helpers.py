@@ -17,11 +17,12 @@ def _bench():
 
 def test_pmc_traffic_found_for_bench_slab():
     b = _bench()
-    t, src = b.pmc_traffic("k_jacobi_lds<8, 1, false>", "4096x4096")
+    t, src, blocks = b.pmc_traffic("k_jacobi_lds<8, 1, false>", "4096x4096")
     assert t is not None and src.startswith("profiles/")
     # one-pass bytes of the launch are 201.3 MB; the measured traffic is within 1.25x
     assert 201326592 <= t <= 1.25 * 201326592
-    assert b.pmc_traffic("k_jacobi_lds<8, 1, false>", "123x45") == (None, None)
+    assert blocks is None   # a one-block kernel: no per-dispatch block count recorded
+    assert b.pmc_traffic("k_jacobi_lds<8, 1, false>", "123x45") == (None, None, None)
 
 
 def test_roofline_valu_is_a_fraction():

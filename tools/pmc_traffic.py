@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--command", default="")
     ap.add_argument("-o", "--out", required=True)
+    ap.add_argument("--persist-blocks", type=int, default=0,
+                    help="T-sweep blocks one k_jacobi_persist dispatch of the profiled run holds "
+                         "(bench.py divides per-dispatch bytes by this, not by its own count)")
+    ap.add_argument("--note", default="")
     a = ap.parse_args()
     fetch, nf = per_dispatch(a.fetch_csv, "FETCH_SIZE")
     write, nw = per_dispatch(a.write_csv, "WRITE_SIZE")
@@ -47,10 +51,14 @@ def main():
         wr = write.get(k, 0.0) * 1024.0
         kernels[k] = {"read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
                       "dispatches": max(nf.get(k, 0), nw.get(k, 0))}
+        if a.persist_blocks and "persist" in k:
+            kernels[k]["blocks_per_dispatch"] = a.persist_blocks
     out = {"workload": a.workload, "command": a.command,
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide streaming reads), "
                          "write = WRITE_SIZE KiB; per dispatch, averaged",
            "kernels": kernels}
+    if a.note:
+        out["note"] = a.note
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     for k, v in kernels.items():

@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--command", default="")
     ap.add_argument("-o", required=True)
+    ap.add_argument("--persist-blocks", type=int, default=0,
+                    help="T-sweep blocks one k_jacobi_persist dispatch of the profiled run holds "
+                         "(bench.py divides per-dispatch figures by this, not by its own count)")
+    ap.add_argument("--note", default="")
     a = ap.parse_args()
     acc = defaultdict(float)
     disp = defaultdict(set)
@@ -33,14 +37,18 @@ def main():
         acc[(k, row["Counter_Name"])] += float(row["Counter_Value"])
         disp[k].add(row["Dispatch_Id"])
     out = {"workload": a.workload, "command": a.command, "kernels": {}}
+    if a.note:
+        out["note"] = a.note
     for k, ids in disp.items():
         n = len(ids)
         out["kernels"][k] = {c: v / n for (kk, c), v in acc.items() if kk == k}
         out["kernels"][k]["dispatches"] = n
+        if a.persist_blocks and "persist" in k:
+            out["kernels"][k]["blocks_per_dispatch"] = a.persist_blocks
     json.dump(out, open(a.o, "w"), indent=1)
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("SQ_INSTS_VALU", 0))[:8]:
         print(f"{k:44s} n={v['dispatches']:4d} " +
-              " ".join(f"{c}={x:.4g}" for c, x in v.items() if c != "dispatches"))
+              " ".join(f"{c}={x:.4g}" for c, x in v.items() if c not in ("dispatches", "blocks_per_dispatch")))
 
 
 if __name__ == "__main__":
