@@ -425,7 +425,8 @@ class Model:
 
     @property
     def jacobi_kernel(self) -> dict:
-        """Kind and rocprofv3 name of the kernel a fixed-count solve launches."""
+        """Kind and rocprofv3 name of the kernel the solve launches (include/cfd.h:
+        5 the LDS row march, 6 the resident tolerance-mode solve, ...)."""
         kind, name = C.c_int(), C.create_string_buffer(96)
         check("cfd_get_jacobi_kernel",
               load().cfd_get_jacobi_kernel(self._hh(), C.byref(kind), name, 96))

@@ -41,7 +41,10 @@ constexpr int kResStride = 16;
 // counter, [2..5] / [6..9] its waves' max |p'| stored in its last even / odd
 // block
 constexpr int kPersistFlagStride = 16;
-constexpr int kPersistHeadLines = 1;
+// head lines: 0 = the persistent solve's words ([1] abort, [2] steals, [3]
+// SUMS blocks); 2 = the resident solve's barrier counter, 4 = its exit ticket
+// (cfd_jacobi_resident.hip; own 128-B lines)
+constexpr int kPersistHeadLines = 5;
 // flag = epoch << kPersistBlockBits | blocks done: room for every block of the
 // longest solve (kMaxSweeps / 8 = 512), epochs below 2^(32 - bits)
 constexpr int kPersistBlockBits = 10;
@@ -218,6 +221,10 @@ void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int pa
                         int out_lo, int out_hi, hipStream_t s);
 void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, int par,
                        hipStream_t s);
+// The whole tolerance-mode solve of a single-domain grid in one launch
+// (cfd_jacobi_resident.hip); false: no tile plan fits (nothing launched).
+bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, hipStream_t s);
+bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *wgs);
 void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
                         hipStream_t s);
 // dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before

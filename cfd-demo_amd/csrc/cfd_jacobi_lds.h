@@ -1067,7 +1067,12 @@ int lds_segments(const Geom &g, int nrows, int nwc, int pad, int occ_override = 
     const int bpc = bpc_cap > 0 ? std::min(occ, bpc_cap) : occ;
     const int wgs_per_col = std::max(1, g.n_cu * bpc / nwc);
     const int per_round = kLdsWaves * wgs_per_col;
-    const int rounds = std::max(1, cdiv(nrows, (long)per_round * kMaxRows));
+    // the persistent launch (occ_override) keeps ONE round whatever the
+    // segment length: a tile per resident workgroup, so no tile waits for an
+    // owner that is not resident (8192^2: two rounds made half the tiles run
+    // by stealing, 274 vs 170 us per block, profiles/r4/prof_r4a)
+    const int rounds =
+        occ_override > 0 ? 1 : std::max(1, cdiv(nrows, (long)per_round * kMaxRows));
     return std::max(1, std::min(per_round * rounds, nrows / kMinRows));
 }
 

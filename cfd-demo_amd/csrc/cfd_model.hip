@@ -1108,7 +1108,38 @@ struct cfd_model {
         const int tmax = g.tol_enabled ? 1 : t_max;
         int launches = 0;   // buffers flip once per launch
         if (!sharded()) {
-            if (spec) {
+            bool resident = false;
+            if (spec && resident_mode()) {
+                // the whole solve in one launch, the early exit decided on the
+                // device; in-process resident / persistent launches of
+                // different models on one device are ordered (all its
+                // workgroups must be resident at once)
+                PersistGate &gate = persist_gate(device);
+                std::lock_guard<std::mutex> lk(gate.mu);
+                if (gate.last && gate.last != stream) {
+                    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                    (void)hipStreamIsCapturing(gate.last, &cs);
+                    if (cs == hipStreamCaptureStatusNone) {
+                        if (!gate.ev) HIP_TRY(hipEventCreateWithFlags(&gate.ev, hipEventDisableTiming));
+                        HIP_TRY(hipEventRecord(gate.ev, gate.last));
+                        HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
+                    }
+                }
+                resident = launch_jacobi_resident(g, f, pass, iters, stream);
+                if (resident) {
+                    gate.last = stream;
+                    // launches the per-launch path would count (host_cur is
+                    // not tracked with the tolerance on; Ctl::spec_launches is)
+                    for (int it = 0; it < iters;) {
+                        int T, lo, hi, exch;
+                        plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
+                        it += T;
+                        ++launches;
+                    }
+                }
+            }
+            if (resident) {
+            } else if (spec) {
                 // the tolerance mode, temporally blocked (speculative): each
                 // launch runs kSpecT sweeps with every sweep's residual, a check
                 // finds the reference's early exit (model.rs:816), and the
@@ -1431,6 +1462,22 @@ struct cfd_model {
         return spec_env && !sharded() && g.tol_enabled &&
                params.pressure_solver == CFD_SOLVER_JACOBI;
     }
+    // The tolerance-mode solve of a small grid as ONE resident launch
+    // (k_jacobi_resident, cfd_jacobi_resident.hip): CFD_RESIDENT=1 on any
+    // grid, 0 never; default on up to kResidentAutoCells cells, where the
+    // per-launch row march is latency-bound.  Off after a timeout.
+    static constexpr long kResidentAutoCells = 1l << 21;
+    int resident_env = [] {
+        const char *e = getenv("CFD_RESIDENT");
+        return e ? atoi(e) : -1;
+    }();
+    bool resident_off = false;
+    bool resident_mode() const {
+        if (resident_env == 0 || resident_off || !spec_mode()) return false;
+        if (resident_env < 0 && (long)g.nx * g.ny > kResidentAutoCells) return false;
+        int br, bc, nt, wg;
+        return jacobi_resident_geometry(g, &br, &bc, &nt, &wg);
+    }
 
     // u* <- u, v* <- v and the divergence at the head of a corrector pass
     // (model.rs:698-704): one fused launch (CFD_COPY_DIV=0: the two launches)
@@ -1668,6 +1715,7 @@ struct cfd_model {
         if (!h_nonfinite || !*(volatile uint32_t *)(h_nonfinite + 2)) return 0;
         *(volatile uint32_t *)(h_nonfinite + 2) = 0u;
         persist_env = false;
+        resident_off = true;
         return fail(CFD_ETIMEOUT, "persistent Jacobi solve timed out waiting for a neighbouring "
                                   "workgroup (not all resident); its result is invalid; "
                                   "per-launch solves from now on");
@@ -2671,12 +2719,15 @@ int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal) {
 int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len) {
     if (!m) return fail(CFD_EINVAL, "null model");
     const bool spec = m->spec_mode();
+    const bool resident = m->resident_mode();
     const int T = spec ? kMaxTemporal : m->g.tol_enabled ? 1 : m->t_max;
-    const int k = spec ? 5 : T <= 1 ? 0 : m->g.tb_kind;
+    const int k = resident ? 6 : spec ? 5 : T <= 1 ? 0 : m->g.tb_kind;
     if (kind) *kind = k;
     if (name && name_len) {
         char buf[96];
-        if (spec)
+        if (resident)
+            snprintf(buf, sizeof buf, "k_jacobi_resident<%d>", m->g.fastdiv);
+        else if (spec)
             snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, 2>", T, m->g.fastdiv);
         else if (k == 0)
             snprintf(buf, sizeof buf, "k_jacobi<%d, %d>", kJacRowsPerWave, m->g.fastdiv);

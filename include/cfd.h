@@ -229,9 +229,12 @@ int cfd_get_halo_depth(const cfd_model *m);
  * for this grid's divisors (0 IEEE, 1 reciprocal multiply, 2 FMA-corrected)
  * and sweeps per launch (1 when the tolerance is on). */
 int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal);
-/* The Jacobi kernel a fixed-count solve launches: kind 0 single sweep
- * (k_jacobi), 1 register-march temporal blocking (k_jacobi_tb), 3 / 4 the
- * prefetch-pipelined march with 4 / 2 columns per lane (k_jacobi_pipe), and
+/* The Jacobi kernel a solve launches: kind 0 single sweep (k_jacobi), 1
+ * register-march temporal blocking (k_jacobi_tb), 3 / 4 the
+ * prefetch-pipelined march with 4 / 2 columns per lane (k_jacobi_pipe), 5 the
+ * LDS row march (k_jacobi_lds; with the tolerance on its speculative form), 6
+ * the tolerance-mode solve of a small grid as one resident launch
+ * (k_jacobi_resident, default up to 2^21 cells; CFD_RESIDENT=0/1 forces), and
  * its instantiated name as rocprofv3 reports it (NUL-terminated, truncated to
  * name_len). */
 int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len);

@@ -48,13 +48,26 @@ def _compare(tag, m, o):
     return int(s.jacobi_sweeps_total)
 
 
+@pytest.fixture(params=["resident", "launches"])
+def solve_form(request, monkeypatch):
+    """Every parity case runs twice: as the small-grid default, the whole
+    solve in one resident launch (k_jacobi_resident), and as the per-launch
+    speculative path (CFD_RESIDENT=0: k_jacobi_lds MODE 2 + checks + redo)."""
+    monkeypatch.setenv("CFD_RESIDENT", "1" if request.param == "resident" else "0")
+    return request.param
+
+
 def _run(grid, params, okw, steps, tag):
     import cfdamd
     from oracle import OracleModel
     c = grid.obstacle
     m = cfdamd.Model(grid, params, device=0)
     assert m.kernel_config["temporal"] == 8, m.kernel_config
-    assert m.jacobi_kernel["name"].startswith("k_jacobi_lds<8,"), m.jacobi_kernel
+    if os.environ.get("CFD_RESIDENT") == "1":
+        assert m.jacobi_kernel["name"].startswith("k_jacobi_resident<"), m.jacobi_kernel
+        assert m.jacobi_kernel["kind"] == 6
+    else:
+        assert m.jacobi_kernel["name"].startswith("k_jacobi_lds<8,"), m.jacobi_kernel
     o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly,
                     cylinder=(c.center_x, c.center_y, c.radius) if c else None, **okw)
     sweeps = []
@@ -72,7 +85,7 @@ def _run(grid, params, okw, steps, tag):
 
 
 @pytest.mark.parametrize("p_tol", [1e-4, 1e-3, 3e-5])
-def test_spec_cavity_parity_mode(p_tol):
+def test_spec_cavity_parity_mode(p_tol, solve_form):
     """128^2 cavity, Re 100, the reference's control flow at three tolerances:
     solves end early at varying sweeps (the re-run with 1..7 sweeps)."""
     import cfdamd
@@ -83,14 +96,14 @@ def test_spec_cavity_parity_mode(p_tol):
     assert any(s % 8 for s in sweeps), sweeps
 
 
-def test_spec_channel_default_grid_cylinder():
+def test_spec_channel_default_grid_cylinder(solve_form):
     """The reference's default grid (800 x 264 channel, cylinder, src/app.rs
     :33-53) with its default parameters (SimulationParams::default)."""
     import cfdamd
     _run(cfdamd.default_grid(), cfdamd.SimulationParams(), {}, 12, "default channel")
 
 
-def test_spec_channel_second_order_parabolic():
+def test_spec_channel_second_order_parabolic(solve_form):
     import cfdamd
     grid = cfdamd.Grid(256, 96, 30.0, 10.0, cfdamd.Cylinder(7.5, 5.0, 1.5))
     params = cfdamd.SimulationParams(velocity_scheme=cfdamd.VelocityScheme.SecondOrder,
@@ -98,7 +111,7 @@ def test_spec_channel_second_order_parabolic():
     _run(grid, params, dict(scheme=1, inlet_profile=1), 20, "channel SO")
 
 
-def test_spec_c2_parity_mode():
+def test_spec_c2_parity_mode(solve_form):
     """C2 (1024^2 cavity, Re 400) in the reference's control flow."""
     import cfdamd
     params = cfdamd.SimulationParams.cavity(400.0, 50)
@@ -172,6 +185,7 @@ def test_spec_fold_matches_check_launch(monkeypatch, p_tol):
     fold) and the default one-workgroup k_spec_check launch give the same bits
     and sweep counts, and the folded form matches the oracle step by step."""
     import cfdamd
+    monkeypatch.setenv("CFD_RESIDENT", "0")   # the fold belongs to the per-launch path
     monkeypatch.setenv("CFD_SPEC_FOLD", "1")
     params = cfdamd.SimulationParams.cavity(100.0, 50, p_tol=p_tol)
     sweeps = _run(cfdamd.cavity_grid(128), params,
@@ -189,3 +203,81 @@ def test_spec_fold_matches_check_launch(monkeypatch, p_tol):
     for f in STATE:
         assert_bitwise(f"spec fold on/off:{f}", states[1][f], states[0][f])
     assert states[0]["jacobi_sweeps_total"] == states[1]["jacobi_sweeps_total"]
+
+
+def test_resident_deadline_fault_is_loud_and_recoverable(monkeypatch):
+    """A barrier wait past the deadline (forced: CFD_PERSIST_DEADLINE_US=0)
+    aborts the resident solve: the next call raises CFD_ETIMEOUT, the model's
+    later solves run per launch, and the caller's checkpoint restores a state
+    from which the steps equal the oracle, sweep counts included."""
+    import cfdamd
+    from cfdamd._lib import CFD_ETIMEOUT, CfdError
+    from oracle import OracleModel
+    monkeypatch.setenv("CFD_RESIDENT", "1")
+    grid = cfdamd.cavity_grid(256, 128)
+    params = cfdamd.SimulationParams.cavity(400.0, 50, p_tol=2e-4)
+    o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly, bc_kind=1, viscosity=1.0 / 400.0,
+                    p_tol=2e-4)
+    m = cfdamd.Model(grid, params, device=0)
+    try:
+        for k in range(3):
+            m.update()
+            o.update()
+            _compare(f"resident before fault {k}", m, o)
+        ckpt = m.get_state()
+        monkeypatch.setenv("CFD_PERSIST_DEADLINE_US", "0")
+        monkeypatch.setenv("CFD_PERSIST_LATE", "3")   # workgroups 1, 4, ... arrive 2 ms late
+        with pytest.raises(CfdError) as ei:
+            for _ in range(5):   # the first barrier wait faults
+                m.update()
+                m.synchronize()
+        assert ei.value.code == CFD_ETIMEOUT, ei.value
+        monkeypatch.delenv("CFD_PERSIST_DEADLINE_US")
+        monkeypatch.delenv("CFD_PERSIST_LATE")
+        m.set_state(**ckpt)
+        assert m.jacobi_kernel["kind"] == 5   # per launch after the fault
+        for k in range(3):
+            m.update()
+            o.update()
+            _compare(f"after resident fault {k}", m, o)
+    finally:
+        m.close()
+
+
+def test_resident_late_workgroups_bitwise(monkeypatch):
+    """Workgroups that reach the first barrier 2 ms late (CFD_PERSIST_LATE=3)
+    hold the others at the barrier and change no bit."""
+    monkeypatch.setenv("CFD_PERSIST_LATE", "3")
+    import cfdamd
+    monkeypatch.setenv("CFD_RESIDENT", "1")
+    params = cfdamd.SimulationParams.cavity(400.0, 50)
+    _run(cfdamd.cavity_grid(1024), params, dict(bc_kind=1, viscosity=0.0025), 3, "C2 late")
+
+
+def test_resident_two_models_interleaved(monkeypatch):
+    """Two models' resident solves enqueued back to back on their own streams
+    (ordered by the device's launch gate) give each model's own sequential
+    bits."""
+    import cfdamd
+    monkeypatch.setenv("CFD_RESIDENT", "1")
+    grids = [cfdamd.cavity_grid(256, 128), cfdamd.default_grid()]
+    params = [cfdamd.SimulationParams.cavity(400.0, 50, p_tol=2e-4), cfdamd.SimulationParams()]
+    alone = []
+    for g, p in zip(grids, params):
+        m = cfdamd.Model(g, p, device=0)
+        m.update_n(8)
+        alone.append(m.get_state())
+        m.close()
+    ms = [cfdamd.Model(g, p, device=0) for g, p in zip(grids, params)]
+    try:
+        for _ in range(8):
+            for m in ms:
+                m.update()   # no synchronisation between the models
+        for m, ref in zip(ms, alone):
+            st = m.get_state()
+            for f in STATE:
+                assert_bitwise(f"interleaved:{f}", st[f], ref[f])
+            assert st["jacobi_sweeps_total"] == ref["jacobi_sweeps_total"]
+    finally:
+        for m in ms:
+            m.close()
