@@ -458,6 +458,14 @@ class Model:
         return int(n.value)
 
     @property
+    def resident_solves(self) -> int:
+        """Tolerance-mode solves enqueued as one resident launch
+        (k_jacobi_resident; cfd_get_resident_solves)."""
+        n = C.c_uint64()
+        check("cfd_get_resident_solves", load().cfd_get_resident_solves(self._hh(), C.byref(n)))
+        return int(n.value)
+
+    @property
     def persist_blocks(self) -> int:
         """8-sweep blocks the last fixed-count solve ran in one persistent
         launch (k_jacobi_persist); 0 when every block had its own launch."""

@@ -106,6 +106,57 @@ __device__ __forceinline__ f2 fdiv2(f2 x, float c, float r) {
     return (f2){fdiv<FAST>(x.x, c, r), fdiv<FAST>(x.y, c, r)};
 }
 
+// End of a pressure solve: how many sweeps ran, which buffer is current, the
+// returned residual (model.rs:816-823), and whether the corrector loop goes on
+// (model.rs:721-723).  Resets the per-sweep slots for the next solve.
+// k_finalize_solve's work (one workgroup of kBlock threads): fold the solve's
+// residual slots into Ctl::err, count the sweeps that ran, flip the current
+// p' buffer, set the next corrector pass's go flag, clear err[].
+__device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields &f, int pass,
+                                                    int iters, int check_break, int flips,
+                                                    int exact_flips) {
+    Ctl *c = f.ctl;
+    __shared__ int go_s;
+    // fold the spread residual slots into err[]: every sweep's with the
+    // tolerance on, only the last one's for a fixed-count solve (the only
+    // sweep that publishes); one wave per sweep, one lane per slot
+    const int k_lo = g.tol_enabled ? 0 : (iters > 0 ? iters - 1 : 0);
+    const int wv = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+    for (int k = k_lo + wv; k < iters; k += nw) {
+        uint32_t *set = f.err_slots + (size_t)k * kResSlots * kResStride;
+        const float v = read_max(set, c->err[k]);
+        if ((threadIdx.x & 63) < kResSlots) set[(threadIdx.x & 63) * kResStride] = 0u;
+        if ((threadIdx.x & 63) == 0) c->err[k] = __float_as_uint(v);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int go = pass < 0 ? 1 : c->go[pass];
+        if (go) {
+            int n = iters;
+            if (g.tol_enabled && iters > 0) {
+                n = 1;
+                while (n < iters && __uint_as_float(c->err[n - 1]) >= g.p_tol) ++n;
+            }
+            const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
+            // one buffer flip per launch: per sweep with the tolerance on,
+            // `flips` (host-known launch count) for fixed-count solves
+            c->cur = (c->cur + (exact_flips == 2 ? c->spec_launches
+                                : (g.tol_enabled && !exact_flips) ? n : flips)) & 1;
+            c->last_p = res;
+            c->red[5] = __float_as_uint(res);   // the step-end all-reduce carries it (slabs)
+            c->n_exec_last = (uint32_t)n;
+            c->sweeps_total += (uint64_t)n;
+        }
+        if (pass >= 0 && pass + 1 <= kMaxPasses)
+            c->go[pass + 1] = (go && !(check_break && g.tol_enabled && c->last_p < g.p_tol)) ? 1 : 0;
+        if (exact_flips == 2) c->spec_stop = c->spec_redo = c->spec_launch = c->spec_launches = 0;
+        go_s = go;
+    }
+    __syncthreads();
+    if (go_s)
+        for (int k = threadIdx.x; k < iters; k += blockDim.x) c->err[k] = 0u;
+}
+
 // One reference Jacobi update (model.rs:775-793) of the 4 consecutive
 // columns a lane holds, C = row j, B = row j-1, T = row j+1, Rh = rhs row j,
 // L0 / R3 = the columns left / right of the chunk.  The arithmetic is the

@@ -223,7 +223,9 @@ void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, 
                        hipStream_t s);
 // The whole tolerance-mode solve of a single-domain grid in one launch
 // (cfd_jacobi_resident.hip); false: no tile plan fits (nothing launched).
-bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, hipStream_t s);
+// fin: its last workgroup also runs k_finalize_solve's body (exact_flips 2).
+bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, int fin,
+                            int check_break, hipStream_t s);
 bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *wgs);
 void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
                         hipStream_t s);

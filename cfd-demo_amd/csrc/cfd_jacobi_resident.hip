@@ -50,19 +50,31 @@
 namespace cfd {
 namespace {
 
-constexpr int kResWaves = 8;   // 512-thread workgroups: 2 waves per SIMD at 1 workgroup per CU
 constexpr int kResMaxT = 8;
 
-template <int FAST>
-__global__ __launch_bounds__(kResWaves * 64) void k_jacobi_resident(
-    Geom g, float *__restrict__ p0, float *__restrict__ p1, const float *__restrict__ rhs, Ctl *ctl,
-    uint32_t *persist, uint32_t *host_fail, int pass, int iters, int T, int BR, int BC, int tiles_x,
-    int ntiles, int res_hi, uint32_t deadline, int late) {
+// WAVES: 8 (512 threads) or 16; ROWS: rows of one column a thread updates
+// per step of its loop (their LDS loads in flight together).  fin: the last workgroup out runs the solve's
+// finalize (k_finalize_solve's body, exact_flips = 2) instead of a launch.
+template <int FAST, int WAVES, int ROWS>
+__global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
+    Geom g, Fields f, int pass, int iters, int T, int BR, int BC, int tiles_x, int ntiles,
+    int res_hi, uint32_t deadline, int late, int fin, int check_break) {
+    constexpr int kResWaves = WAVES;
     extern __shared__ float lds_dyn[];
     __shared__ float red_s[kResWaves][kResMaxT];
-    __shared__ int flag_s;   // abort (1) after the barrier
+    __shared__ int flag_s;   // abort (1) after the barrier; last workgroup out at the end
     __shared__ uint32_t err_s[kResMaxT];
-    if (pass_off(ctl, pass)) return;
+    Ctl *const ctl = f.ctl;
+    float *const p0 = f.pp[0], *const p1 = f.pp[1];
+    const float *__restrict__ rhs = f.rhs;
+    uint32_t *const persist = f.persist;
+    uint32_t *const host_fail = f.host_nonfinite ? f.host_nonfinite + 2 : nullptr;
+    if (pass_off(ctl, pass)) {
+        // the pass does not run: its finalize still closes the corrector loop
+        // (go[pass + 1] = 0)
+        if (fin && blockIdx.x == 0) solve_finalize_body(g, f, pass, iters, check_break, 0, 2);
+        return;
+    }
     uint32_t *const abortw = persist + 1;
     uint32_t *const bar = persist + 2 * kPersistFlagStride;
     uint32_t *const ticket = persist + 4 * kPersistFlagStride;
@@ -79,6 +91,12 @@ __global__ __launch_bounds__(kResWaves * 64) void k_jacobi_resident(
     const float om1 = 1.0f - omega;
     const int cur0 = ctl->cur;
 
+    // The tile's LDS region is its output cells plus a T-cell halo (clamped
+    // to the grid), the same for every block, so with one tile per workgroup
+    // the rhs region is loaded once per solve (rhs is constant in a solve).
+    const bool keep_rhs = ntiles <= G;
+    bool rhs_in = false;
+    constexpr int NT = kResWaves * 64;
     // Tb sweeps of every tile of this workgroup from `src` into `dst`;
     // publish: fold each sweep's residual into red_s[wave][s]
     auto run_tiles = [&](const float *__restrict__ src, float *__restrict__ dst, int Tb,
@@ -87,41 +105,84 @@ __global__ __launch_bounds__(kResWaves * 64) void k_jacobi_resident(
             const int ty = t / tiles_x, tx = t - ty * tiles_x;
             const int r0 = ty * BR, r1 = min(ny, r0 + BR);
             const int c0 = tx * BC, c1 = min(nx, c0 + BC);
-            const int R0 = max(0, r0 - Tb), R1 = min(ny, r1 + Tb);
-            const int C0 = max(0, c0 - Tb), C1 = min(nx, c1 + Tb);
-            const int W = C1 - C0;
+            const int R0 = max(0, r0 - T), R1 = min(ny, r1 + T);
+            const int C0 = max(0, c0 - T), C1 = min(nx, c1 + T);
+            const int W = C1 - C0, H = R1 - R0;
+            const bool ld_rhs = !(keep_rhs && rhs_in);
+            rhs_in = true;
             __syncthreads();   // the previous tile's LDS reads are done
-            for (int r = R0 + wave; r < R1; r += kResWaves)
-                for (int c = C0 + lane; c < C1; c += 64) {
-                    const int i = (r - R0) * W + (c - C0);
-                    LA[i] = src[(size_t)r * nx + c];
-                    LR[i] = rhs[(size_t)r * nx + c];
+            {
+                // flat over the region, 4 loads in flight per thread before
+                // their LDS stores; row = idx / W by a float reciprocal (exact
+                // for these sizes: idx < 2^13)
+                const float rW = 1.0f / (float)W;
+                const int n = H * W;
+                for (int i0 = (int)threadIdx.x; i0 < n; i0 += 4 * NT) {
+                    float pv[4], rv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = i0 + u * NT;
+                        const int rr = (int)(((float)i + 0.5f) * rW);
+                        const size_t gi = (size_t)(R0 + rr) * nx + (C0 + i - rr * W);
+                        pv[u] = i < n ? src[gi] : 0.0f;
+                        rv[u] = (i < n && ld_rhs) ? rhs[gi] : 0.0f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = i0 + u * NT;
+                        if (i < n) {
+                            LA[i] = pv[u];
+                            if (ld_rhs) LR[i] = rv[u];
+                        }
+                    }
                 }
+            }
             __syncthreads();
             float *A = LA, *B = LB;
-            const bool edge = r0 - Tb <= 0 || r1 + Tb >= ny || c0 - Tb <= 0 || c1 + Tb >= nx;
+            const bool edge = r0 - T <= 0 || r1 + T >= ny || c0 - T <= 0 || c1 + T >= nx;
             for (int s = 0; s < Tb; ++s) {
                 const int e = Tb - 1 - s;   // the box this sweep must cover: outputs + e
                 const int br0 = max(0, r0 - e), br1 = min(ny, r1 + e);
                 const int bc0 = max(0, c0 - e), bc1 = min(nx, c1 + e);
-                // interior cells (model.rs:775-793, operation for operation)
+                // interior cells (model.rs:775-793, operation for operation),
+                // ROWS consecutive rows of one column per thread: their loads
+                // issue together (rows past the region clamp to its last row;
+                // those values feed no stored cell)
                 const int ir0 = max(br0, 1), ir1 = min(br1, ny - 1);
                 const int ic0 = max(bc0, 1), ic1 = min(bc1, nx - 1);
                 float ms = 0.0f;
-                for (int r = ir0 + wave; r < ir1; r += kResWaves) {
-                    const bool own_r = publish && r >= r0 && r < r1;
+                const int nrg = (ir1 - ir0 + ROWS - 1) / ROWS;
+                for (int q = wave; q < nrg; q += kResWaves) {
+                    const int rb = ir0 + q * ROWS;
                     for (int c = ic0 + lane; c < ic1; c += 64) {
-                        const int i = (r - R0) * W + (c - C0);
-                        const float center = A[i];
-                        const float horizontal = fdiv<FAST>(A[i + 1] + A[i - 1], dx_sq, r_dx_sq);
-                        const float vertical = fdiv<FAST>(A[i + W] + A[i - W], dy_sq, r_dy_sq);
-                        const float p_update =
-                            fdiv<FAST>(horizontal + vertical - LR[i], denom, r_denom);
-                        const float nv = omega * p_update + om1 * center;
-                        B[i] = nv;
-                        if (own_r && c >= c0 && c < c1 && c < res_hi) {
-                            const float d = fabsf(nv - center);
-                            ms = d > ms ? d : ms;   // NaN-ignoring, like reduce_max
+                        const int cc = c - C0;
+                        float col[ROWS + 2], lf[ROWS], rt[ROWS], rh[ROWS];
+#pragma unroll
+                        for (int k = 0; k < ROWS + 2; ++k)
+                            col[k] = A[(min(rb - 1 + k, R1 - 1) - R0) * W + cc];
+#pragma unroll
+                        for (int k = 0; k < ROWS; ++k) {
+                            const int i = (min(rb + k, R1 - 1) - R0) * W + cc;
+                            lf[k] = A[i - 1];
+                            rt[k] = A[i + 1];
+                            rh[k] = LR[i];
+                        }
+#pragma unroll
+                        for (int k = 0; k < ROWS; ++k) {
+                            const int r = rb + k;
+                            if (r < ir1) {
+                                const float center = col[k + 1];
+                                const float horizontal = fdiv<FAST>(rt[k] + lf[k], dx_sq, r_dx_sq);
+                                const float vertical = fdiv<FAST>(col[k + 2] + col[k], dy_sq, r_dy_sq);
+                                const float p_update =
+                                    fdiv<FAST>(horizontal + vertical - rh[k], denom, r_denom);
+                                const float nv = omega * p_update + om1 * center;
+                                B[(r - R0) * W + cc] = nv;
+                                if (publish && r >= r0 && r < r1 && c >= c0 && c < c1 && c < res_hi) {
+                                    const float d = fabsf(nv - center);
+                                    ms = d > ms ? d : ms;   // NaN-ignoring, like reduce_max
+                                }
+                            }
                         }
                     }
                 }
@@ -246,41 +307,71 @@ __global__ __launch_bounds__(kResWaves * 64) void k_jacobi_resident(
         it += Tb;
         ++k;
     }
+    if (aborted) return;
+    if (!fin && wg == 0 && threadIdx.x == 0) ctl->spec_launches = blocks;   // k_finalize_solve's flips
+    // the last workgroup out: every arrival is in; zero the counters for the
+    // next launch and (fin) finalize the solve
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (threadIdx.x == 0) {
-        if (wg == 0 && !aborted) ctl->spec_launches = blocks;   // k_finalize_solve's buffer flips
-        if (!aborted &&
-            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                (uint32_t)G - 1u) {
-            // the last workgroup out: every arrival is in, zero for the next launch
+        const bool lastwg =
+            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)G - 1u;
+        if (lastwg) {
             __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (fin) {
+                ctl->spec_launches = blocks;   // every workgroup ran the same blocks
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every err[] atomic is in
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
+        flag_s = lastwg;
     }
+    __syncthreads();
+    if (fin && flag_s) solve_finalize_body(g, f, pass, iters, check_break, 0, 2);
 }
 
 struct ResidentPlan {
     int BR, BC, tiles_x, ntiles, G, lds;
 };
+// CFD_RESIDENT_TILE=<rows>x<cols> forces the tile shape (measurement)
 
 inline int resident_lds_bytes(int BR, int BC, int T) { return 3 * (BR + 2 * T) * (BC + 2 * T) * 4; }
+
+// 8 waves (512 threads) by default: the occupancy query admits two per CU
+// (the residency rule above); CFD_RESIDENT_WAVES=16 asks for 1,024-thread
+// workgroups, taken only where two of those fit a CU as well
+inline int resident_waves() {
+    const char *e = getenv("CFD_RESIDENT_WAVES");
+    return e && atoi(e) == 16 ? 16 : 8;
+}
 
 template <int FAST>
 int resident_blocks_per_cu(int lds) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &n, reinterpret_cast<const void *>(&k_jacobi_resident<FAST>), kResWaves * 64, lds) !=
-        hipSuccess)
+    const void *k = resident_waves() == 8
+                        ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 2>)
+                        : reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 16, 2>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, resident_waves() * 64, lds) != hipSuccess)
         return 0;
     return n;
 }
 
 // Tile shape: the candidate with the least LDS-box work per workgroup
 // (ceil(tiles / G) x box cells), every candidate admitting 2 workgroups per CU.
+// Single domain only (rows 0..ny-1 owned; the fields' ghost rows unused).
 bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
-    static const int cand[][2] = {{8, 64}, {16, 64}, {16, 128}, {32, 96}};
+    if (g.nx < 4 || g.ny < 4 || g.j0 != 0 || g.nyl != g.ny) return false;
+    // box widths BC + 2e (e = 0..T-1) fill 64-lane passes: BC = 48 -> 48..62
+    // columns in one pass, 112 -> 112..126 in two
+    static const int cand[][2] = {{8, 48}, {16, 48}, {32, 48}, {16, 112}, {32, 112}};
     long best = -1;
     for (const auto &cd : cand) {
-        const int BR = cd[0], BC = cd[1];
+        int BR = cd[0], BC = cd[1];
+        if (const char *te = getenv("CFD_RESIDENT_TILE")) {
+            if (sscanf(te, "%dx%d", &BR, &BC) != 2 || BR < 2 || BC < 2) return false;
+            if (&cd != &cand[0]) break;
+        }
         const int lds = resident_lds_bytes(BR, BC, T);
         const int occ = g.fastdiv == 1   ? resident_blocks_per_cu<1>(lds)
                         : g.fastdiv == 2 ? resident_blocks_per_cu<2>(lds)
@@ -307,34 +398,54 @@ static int resident_simd_end(int nx) {
     return e;
 }
 
-bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, hipStream_t s) {
-    if (iters <= 0 || g.nx < 4 || g.ny < 4 || g.hg != 0 || g.j0 != 0 || g.nyl != g.ny) return false;
-    const int T = kResMaxT;
+// sweeps per block between barriers (CFD_RESIDENT_T, 2..8; default 8)
+static int resident_T() {
+    const char *e = getenv("CFD_RESIDENT_T");
+    return e ? std::max(2, std::min(kResMaxT, atoi(e))) : kResMaxT;
+}
+
+bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, int fin,
+                            int check_break, hipStream_t s) {
+    if (iters <= 0) return false;
+    const int T = resident_T();
     ResidentPlan p;
     if (!resident_plan(g, T, &p)) return false;
     const char *de = getenv("CFD_PERSIST_DEADLINE_US");
     const double dl_us = de ? std::max(0.0, atof(de)) : 10e6;
     const uint32_t deadline = (uint32_t)std::min(4.0e9, dl_us * 100.0);
-    uint32_t *hf = f.host_nonfinite ? f.host_nonfinite + 2 : nullptr;
     const char *le = getenv("CFD_PERSIST_LATE");
     const int late = le ? std::max(0, atoi(le)) : 0;
-#define CFD_RES_LAUNCH(FASTV)                                                                      \
-    hipLaunchKernelGGL((k_jacobi_resident<FASTV>), dim3(p.G), dim3(kResWaves * 64), p.lds, s, g,   \
-                       f.pp[0], f.pp[1], f.rhs, f.ctl, f.persist, hf, pass, iters, T, p.BR, p.BC,     \
-                       p.tiles_x, p.ntiles, resident_simd_end(g.nx), deadline, late)
-    if (g.fastdiv == 1)
-        CFD_RES_LAUNCH(1);
-    else if (g.fastdiv == 2)
-        CFD_RES_LAUNCH(2);
-    else
-        CFD_RES_LAUNCH(0);
+    const char *re = getenv("CFD_RESIDENT_ROWS");
+    const int rows = re ? atoi(re) : 2;
+#define CFD_RES_LAUNCH(FASTV, WV, RW)                                                              \
+    hipLaunchKernelGGL((k_jacobi_resident<FASTV, WV, RW>), dim3(p.G), dim3(WV * 64), p.lds, s, g, \
+                       f, pass, iters, T, p.BR, p.BC, p.tiles_x, p.ntiles,                        \
+                       resident_simd_end(g.nx), deadline, late, fin, check_break)
+#define CFD_RES_WAVES(FASTV)                \
+    if (resident_waves() == 16)             \
+        CFD_RES_LAUNCH(FASTV, 16, 2);       \
+    else if (rows == 1)                     \
+        CFD_RES_LAUNCH(FASTV, 8, 1);        \
+    else if (rows == 4)                     \
+        CFD_RES_LAUNCH(FASTV, 8, 4);        \
+    else                                    \
+        CFD_RES_LAUNCH(FASTV, 8, 2);
+    if (g.fastdiv == 1) {
+        CFD_RES_WAVES(1)
+    } else if (g.fastdiv == 2) {
+        CFD_RES_WAVES(2)
+    } else {
+        CFD_RES_WAVES(0)
+    }
+#undef CFD_RES_WAVES
 #undef CFD_RES_LAUNCH
     return true;
 }
 
 bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *wgs) {
+    // (the tile plan the launch would take; false: none fits)
     ResidentPlan p;
-    if (!resident_plan(g, kResMaxT, &p)) return false;
+    if (!resident_plan(g, resident_T(), &p)) return false;
     *br = p.BR;
     *bc = p.BC;
     *tiles = p.ntiles;

@@ -1107,8 +1107,8 @@ struct cfd_model {
         const bool spec = spec_mode();
         const int tmax = g.tol_enabled ? 1 : t_max;
         int launches = 0;   // buffers flip once per launch
+        bool resident = false;   // the resident launch also finalizes the solve
         if (!sharded()) {
-            bool resident = false;
             if (spec && resident_mode()) {
                 // the whole solve in one launch, the early exit decided on the
                 // device; in-process resident / persistent launches of
@@ -1125,8 +1125,9 @@ struct cfd_model {
                         HIP_TRY(hipStreamWaitEvent(stream, gate.ev, 0));
                     }
                 }
-                resident = launch_jacobi_resident(g, f, pass, iters, stream);
+                resident = launch_jacobi_resident(g, f, pass, iters, 1, pass >= 1 ? 1 : 0, stream);
                 if (resident) {
+                    ++resident_solves;
                     gate.last = stream;
                     // launches the per-launch path would count (host_cur is
                     // not tracked with the tolerance on; Ctl::spec_launches is)
@@ -1317,7 +1318,9 @@ struct cfd_model {
             }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps + halo rounds
         }
-        if (defer_finalize) {
+        if (resident) {
+            // k_jacobi_resident's last workgroup finalized the solve
+        } else if (defer_finalize) {
             // the corrector finish's workgroup 0 does it (one launch less)
             fin_deferred = SolveFinalizeArgs{f.pp[(host_cur + launches) & 1], pass, iters,
                                              pass >= 1 ? 1 : 0, launches};
@@ -1472,11 +1475,16 @@ struct cfd_model {
         return e ? atoi(e) : -1;
     }();
     bool resident_off = false;
+    uint64_t resident_solves = 0;   // resident launches enqueued (cfd_get_resident_solves)
     bool resident_mode() const {
         if (resident_env == 0 || resident_off || !spec_mode()) return false;
         if (resident_env < 0 && (long)g.nx * g.ny > kResidentAutoCells) return false;
         int br, bc, nt, wg;
-        return jacobi_resident_geometry(g, &br, &bc, &nt, &wg);
+        if (!jacobi_resident_geometry(g, &br, &bc, &nt, &wg)) return false;
+        // by default one tile per workgroup (C2's 1024^2 needs 2-3 per
+        // workgroup and ran 3.65 -> 7.07 ms per step resident,
+        // profiles/r4/ab_c2_r4j.log)
+        return resident_env > 0 || nt <= wg;
     }
 
     // u* <- u, v* <- v and the divergence at the head of a corrector pass
@@ -2778,6 +2786,12 @@ int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks) {
     uint32_t v = 0;
     HIP_TRY(hipMemcpy(&v, m->f.persist + 3, 4, hipMemcpyDeviceToHost));
     *blocks = v;
+    return 0;
+}
+
+int cfd_get_resident_solves(const cfd_model *m, uint64_t *solves) {
+    if (!m || !solves) return fail(CFD_EINVAL, "null argument");
+    *solves = m->resident_solves;
     return 0;
 }
 

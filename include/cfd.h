@@ -253,6 +253,9 @@ int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
  * taken only where a per-task guard proves it bitwise (k_jacobi_persist) --
  * summed over the model's life.  Synchronises.  (new; diagnostics) */
 int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
+/* Tolerance-mode solves this model enqueued as one resident launch
+ * (k_jacobi_resident, see cfd_get_jacobi_kernel kind 6); diagnostics. */
+int cfd_get_resident_solves(const cfd_model *m, uint64_t *solves);
 /* The tile geometry of the model's 8-sweep kind-5 Jacobi launch over its
  * first block's rows (persist != 0: the persistent form's): the dynamic LDS
  * pad in bytes (24 KiB caps a CU at 3 four-wave workgroups on cache-resident

@@ -79,6 +79,11 @@ def _run(grid, params, okw, steps, tag):
             tot = _compare(f"{tag} step {k + 1}", m, o)
             sweeps.append(tot - prev)
             prev = tot
+        # the form that ran, from the device: resident solves launched
+        if os.environ.get("CFD_RESIDENT") == "1":
+            assert m.resident_solves >= steps, (m.resident_solves, steps)
+        elif os.environ.get("CFD_RESIDENT") == "0":
+            assert m.resident_solves == 0
     finally:
         m.close()
     return sweeps
