@@ -155,6 +155,10 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
     __syncthreads();
     if (go_s)
         for (int k = threadIdx.x; k < iters; k += blockDim.x) c->err[k] = 0u;
+    // the next solve's SUMS guard chain starts from empty sets
+    if (f.guard_slots)
+        for (int q = threadIdx.x; q < kGuardSets * kResSlots; q += blockDim.x)
+            f.guard_slots[(size_t)(q / kResSlots) * kResSlots * kResStride + (q % kResSlots) * kResStride] = 0u;
 }
 
 // One reference Jacobi update (model.rs:775-793) of the 4 consecutive

@@ -51,7 +51,11 @@ constexpr int kPersistBlockBits = 10;
 static_assert((1 << kPersistBlockBits) > kMaxSweeps / 8, "persistent flag layout");
 constexpr int kPersistMaxGroups = 16384;   // tiles (wave columns x row groups)
 constexpr size_t kPersistWords = (size_t)(kPersistMaxGroups + kPersistHeadLines) * kPersistFlagStride;
-constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 8) * kResSlots * kResStride + kPersistWords;
+// slot sets: kMaxSweeps per-sweep residual sets, then red (4), vis (2), 2
+// spare, the SUMS guard of the per-launch solve (kGuardSets, from +8), 3 spare;
+// then the persistent solve's words
+constexpr int kGuardSets = 5;
+constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 16) * kResSlots * kResStride + kPersistWords;
 
 // Device-resident control block: every data-dependent decision of
 // Model::update lives here so a whole step can be enqueued (or replayed as a
@@ -118,6 +122,8 @@ struct Geom {
     int32_t pred_div;     // predictors + divergence: 2: one row march (k_predict_march, both
                           // schemes), 1: fused 2-row tile (k_predict_div, first order),
                           // 0: separate launches; where the fused forms apply
+    int32_t guard_par0;   // r4: the solve's first k_jacobi_lds launch index of a guarded
+                          // chain (the SUMS form's guard, Fields::guard_slots); -1: none
 };
 
 struct Fields {
@@ -141,6 +147,11 @@ struct Fields {
     // the RCCL watchdog's evidence of forward progress
     uint32_t *host_progress;
     uint32_t *persist;   // kPersistWords words after the slot sets (see kPersistFlagStride)
+    // r4: the per-launch solve's SUMS guard, kGuardSets spread sets: sets 0..3
+    // a ring of max |p'| the chain's launch g stores (set g & 3), set 4 max
+    // |rhs| (its first launch); zeroed by every solve's finalize.  Word 0 of
+    // set kGuardSets counts launches run in the SUMS form (diagnostics)
+    uint32_t *guard_slots;
 };
 
 // ---- launchers (cfd_kernels.hip) ----

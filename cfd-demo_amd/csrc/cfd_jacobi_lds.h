@@ -29,6 +29,7 @@
 // update is explicit packed f32 arithmetic on column pairs.
 #pragma once
 #include <cmath>
+#include <type_traits>
 
 #include "cfd_device.h"
 
@@ -116,7 +117,10 @@ constexpr int ring_depth(int T, int PD, int G) {
 // overflow included; a subnormal h + v is exact).  k_jacobi_persist proves
 // that bound per task before it picks SUMS (its guard); otherwise, and for
 // every other launch, the reference's form runs.
-template <int T, int FAST, int MODE, bool SUMS = false>
+// GRD (r4, per-launch solves on a single domain, k_jacobi_lds): 1 = a launch
+// of a guarded chain, tracks max |p'| of what it stores (omax, the next
+// launch's guard); 2 = the chain's first launch, also max |rhs| (rmax).
+template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1 || MODE == 5, SPEC = MODE == 2, REDO = MODE == 3;
     // MODE 4 (PERSIST): a block of k_jacobi_persist; p' moves between
@@ -131,8 +135,9 @@ struct LdsMarch {
 #ifndef CFD_PROBE_NOTRACK
 #define CFD_PROBE_NOTRACK 0   // (diagnostic builds: no guard tracking)
 #endif
-    static constexpr bool TRACK_IN = PERSIST && !SUMS && !CFD_PROBE_NOTRACK;
-    static_assert(!SUMS || (FAST == 1 && PERSIST), "SUMS: persistent, reciprocal multiply");
+    static constexpr bool TRACK_IN = (PERSIST && !SUMS && !CFD_PROBE_NOTRACK) || GRD == 2;
+    static constexpr bool TRACK_OUT = (PERSIST && !CFD_PROBE_NOTRACK) || GRD > 0;
+    static_assert(!SUMS || FAST == 1, "SUMS: reciprocal multiply");
     static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
     static constexpr int PST_AUX = PERSIST ? 16 : CFD_LDS_ST_AUX;
     // Stage s of slot v computes row k - s - off(s).  With G = 1 (off = 0)
@@ -180,6 +185,37 @@ struct LdsMarch {
     float mm[SPEC ? T : 1];   // SPEC: stage s's residual (segment rows only)
     int r0v, r1v;             // the segment's output rows (march order)
     int nst;                  // REDO: stages to run (< T)
+    int nyl_;
+
+    LdsMarch() = default;
+    // the same march state in the other form (the chain guard's SUMS twin,
+    // lds_block): member by member, so the state stays in registers
+    template <bool S2, int G2>
+    __device__ __forceinline__ explicit LdsMarch(const LdsMarch<T, FAST, MODE, S2, G2> &o) {
+#pragma unroll
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+            for (int b = 0; b < NW; ++b) W[a][b] = o.W[a][b];
+#pragma unroll
+        for (int q = 0; q < PD; ++q) {
+            PQ[q] = o.PQ[q];
+            RQ[q] = o.RQ[q];
+        }
+        ring = o.ring;
+        lane = o.lane;
+        k_first = o.k_first, S = o.S, lo_clamp = o.lo_clamp, hi_clamp = o.hi_clamp, nch = o.nch;
+        g_first = o.g_first, g_last = o.g_last, g_top = o.g_top, g_zero = o.g_zero;
+        row_bytes = o.row_bytes, wbase = o.wbase;
+        ch = o.ch, vo_ld = o.vo_ld, vo_st = o.vo_st, abase = o.abase, dir = o.dir;
+        e0 = o.e0, e1 = o.e1;
+        dx_sq = o.dx_sq, r_dx_sq = o.r_dx_sq, dy_sq = o.dy_sq, r_dy_sq = o.r_dy_sq;
+        denom = o.denom, r_denom = o.r_denom;
+        rs_p = o.rs_p, rs_r = o.rs_r, rs_d = o.rs_d;
+        m = o.m, omax = o.omax, imax = o.imax, rmax = o.rmax;
+#pragma unroll
+        for (int q = 0; q < (SPEC ? T : 1); ++q) mm[q] = o.mm[q];
+        r0v = o.r0v, r1v = o.r1v, nst = o.nst, nyl_ = o.nyl_;
+    }
 
     __device__ __forceinline__ int act(int vrow) const { return abase + dir * vrow; }
 
@@ -343,12 +379,11 @@ struct LdsMarch {
 #ifndef CFD_PROBE_NOOMAX
 #define CFD_PROBE_NOOMAX 0
 #endif
-                if constexpr (PERSIST && !CFD_PROBE_NOTRACK && !CFD_PROBE_NOOMAX)
+                if constexpr (TRACK_OUT && !CFD_PROBE_NOOMAX)
                     omax = fmaxf(fmaxf(omax, fabsf(n.x)), fabsf(n.y));
             }
         }
     }
-    int nyl_;
 
     template <int V_, int E>
     __device__ __forceinline__ void warmup() {
@@ -429,14 +464,16 @@ struct LdsMarch {
 // trk (persistent blocks): per wave, trk[3 w .. 3 w + 2] = max |p'| of the
 // rows it stored, of the p' rows it loaded and of the rhs rows it used (the
 // last two only in the reference's form; 0 where not tracked or no rows).
-template <int T, int FAST, int MODE, bool SUMS = false>
+template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
 __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           float *__restrict__ pb, const float *__restrict__ rhs,
                                           Ctl *ctl, uint32_t *res_slots, int par, int out_lo,
                                           int out_hi, int nwc, int nseg, int wlo, int whi, f2 *lds,
                                           int nst, int bid, int spec_fold = 0,
-                                          float *trk = nullptr) {
-    using M = LdsMarch<T, FAST, MODE, SUMS>;
+                                          float *trk = nullptr, uint32_t *gset = nullptr,
+                                          uint32_t *grhs = nullptr, const uint32_t *gprev = nullptr,
+                                          float plim = 0.0f, float rlim = 0.0f) {
+    using M = LdsMarch<T, FAST, MODE, SUMS, GRD>;
     constexpr bool RES = M::RES;
     M w;
     w.nst = nst;
@@ -535,16 +572,30 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         w.PQ[q] = w.template ld<M::PLD_AUX>(w.rs_p, w.k_first + q);
         w.RQ[q] = w.ld(w.rs_r, w.k_first + q);
     }
+    // the march and what the launch publishes; `wx` is w, or (gprev) its
+    // SUMS-form twin (same members) when the chain guard allows it
+    auto finish = [&](auto &wx) {
+    using MX = typename std::remove_reference<decltype(wx)>::type;
     if (row_edge)
-        w.template run<M::kCol | M::kRow>();
+        wx.template run<MX::kCol | MX::kRow>();
     else if (col_edge)
-        w.template run<M::kCol>();
+        wx.template run<MX::kCol>();
     else
-        w.template run<0>();
+        wx.template run<0>();
+    if constexpr (GRD > 0) {
+        // the guard chain: this launch's stored maximum (and the solve's
+        // rhs maximum), one spread slot per wave
+        const float o = wave_max(out_lane ? wx.omax : 0.0f);
+        if (lane == 0) publish_max(gset, bid * kLdsWaves + wave, o);
+        if constexpr (GRD == 2) {
+            const float rm = wave_max(wx.rmax);
+            if (lane == 0) publish_max(grhs, bid * kLdsWaves + wave, rm);
+        }
+    }
     if (M::PERSIST && trk) {
-        const float o = wave_max(out_lane ? w.omax : 0.0f);
-        const float im = M::TRACK_IN ? wave_max(w.imax) : 0.0f;
-        const float rm = M::TRACK_IN ? wave_max(w.rmax) : 0.0f;
+        const float o = wave_max(out_lane ? wx.omax : 0.0f);
+        const float im = M::TRACK_IN ? wave_max(wx.imax) : 0.0f;
+        const float rm = M::TRACK_IN ? wave_max(wx.rmax) : 0.0f;
         if (lane == 0) {
             trk[3 * wave] = o;
             trk[3 * wave + 1] = im;
@@ -557,7 +608,7 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         unsigned acc = 0u;
 #pragma unroll
         for (int s = 0; s < T; ++s) {
-            const float ms = wave_max(out_lane ? w.mm[s] : 0.0f);
+            const float ms = wave_max(out_lane ? wx.mm[s] : 0.0f);
             if (lane == 0 && ms > 0.0f) {
                 uint32_t *slot = res_slots + (size_t)s * kResSlots * kResStride +
                                  ((bid * kLdsWaves + wave) & (kResSlots - 1)) * kResStride;
@@ -571,8 +622,26 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         if (spec_fold) asm volatile("s_waitcnt vmcnt(0)" ::"v"(acc) : "memory");
     }
     if (!RES) return;
-    const float m = wave_max(out_lane ? w.m : 0.0f);
+    const float m = wave_max(out_lane ? wx.m : 0.0f);
     if (lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, m);
+    };
+    if constexpr (FAST == 1 && GRD == 1 && !SUMS && !M::PERSIST) {
+        if (gprev) {
+            // the chain guard's two maxima, loaded while the prefetch is in
+            // flight (one global round trip for both)
+            const int gl = lane & (kResSlots - 1);
+            const float pin = wave_max(__uint_as_float(gprev[gl * kResStride]));
+            const float rin = wave_max(__uint_as_float(grhs[gl * kResStride]));
+            if (pin < plim && rin < rlim) {
+                if (bid == 0 && threadIdx.x == 0)   // diagnostics: launches in the SUMS form
+                    atomicAdd(grhs + (size_t)kResSlots * kResStride, 1u);   // set kGuardSets
+                LdsMarch<T, FAST, MODE, true, GRD> w1(w);
+                finish(w1);
+                return;
+            }
+        }
+    }
+    finish(w);
 }
 
 // Minimum waves per SIMD the register allocation must allow (the SPEC
@@ -639,7 +708,7 @@ template <int T, int FAST, int MODE>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
-    int wlo, int whi, int it, int spec_fold) {
+    int wlo, int whi, int it, int spec_fold, int sums, float plim, float rlim, uint32_t *gslots) {
     using M = LdsMarch<T, FAST, MODE>;
     [[maybe_unused]] constexpr bool RES = M::RES;   // the stamp guard's
     __shared__ f2 lds[kLdsWaves * M::D * 64];
@@ -672,6 +741,55 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         nst = ctl->spec_redo;
         if (nst <= 0) return;
         par = ctl->spec_launch;   // re-run that launch: same source, same destination
+    }
+    if constexpr (FAST == 1 && (MODE == 0 || MODE == 1 || MODE == 2)) {
+        // The SUMS form on a guarded chain of launches (single domain; sums:
+        // the grid allows the form at all, see LdsMarch).  Launch g of the
+        // chain reads exactly what launch g-1 stored (every p' cell, boundary
+        // rows and columns included, is rewritten by every launch), so
+        // max |input| = launch g-1's published max |store|; the chain's
+        // first launch runs the reference's form and measures max |rhs| (rhs
+        // is constant in a solve).  Bounds as k_jacobi_persist's guard:
+        // inputs < plim = 2^124 / R and rhs < rlim = 2^124 keep every value
+        // the T sweeps form below 2^126 / R.  NaN propagates the same operand
+        // in either form (max is NaN-ignoring); +-Inf fails the guard.
+        const int gp = par - g.guard_par0;
+        if (sums && g.guard_par0 >= 0 && gp >= 0) {
+            constexpr size_t kSet = (size_t)kResSlots * kResStride;
+            uint32_t *own = gslots + (size_t)(gp & 3) * kSet;
+            if (blockIdx.x == 0 && threadIdx.x < kResSlots)   // the set launch g+2 will fill
+                gslots[(size_t)((gp + 2) & 3) * kSet + threadIdx.x * kResStride] = 0u;
+            const int bid = xcd_block(g);
+            if (gp == 0) {
+                lds_block<T, FAST, MODE, false, 2>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
+                                                   nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
+                                                   nullptr, own, gslots + 4 * kSet);
+            } else if constexpr (MODE != 2) {
+                // the guard is decided inside (lds_block: its loads overlap the prefetch)
+                lds_block<T, FAST, MODE, false, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
+                                                   nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
+                                                   nullptr, own, gslots + 4 * kSet,
+                                                   gslots + (size_t)((gp - 1) & 3) * kSet, plim, rlim);
+            } else {
+                // the speculative launch (5 waves per SIMD: 96 registers) decides
+                // first: both forms' state live across the decision spills there
+                const float pin = read_max(gslots + (size_t)((gp - 1) & 3) * kSet, 0u);
+                const float rin = read_max(gslots + 4 * kSet, 0u);
+                if (pin < plim && rin < rlim) {
+                    if (blockIdx.x == 0 && threadIdx.x == 0)   // diagnostics: SUMS launches
+                        atomicAdd(gslots + (size_t)kGuardSets * kSet, 1u);
+                    lds_block<T, FAST, MODE, true, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo,
+                                                      out_hi, nwc, nseg, wlo, whi, lds, nst, bid,
+                                                      spec_fold, nullptr, own);
+                } else {
+                    lds_block<T, FAST, MODE, false, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo,
+                                                       out_hi, nwc, nseg, wlo, whi, lds, nst, bid,
+                                                       spec_fold, nullptr, own);
+                }
+            }
+            if (M::SPEC && spec_fold) spec_check_tail<T>(g, ctl, res_slots, it, par);
+            return;
+        }
     }
     lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc, nseg, wlo,
                              whi, lds, nst, xcd_block(g), spec_fold);
@@ -1096,9 +1214,27 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
     const int spec_fold = MODE == 2 && spec_fold_on() ? 1 : 0;
+    // the guarded SUMS form (k_jacobi_lds): reciprocal multiply, dx^2 ==
+    // dy^2 with a power-of-two reciprocal R >= 1, single domain, a chain set
+    // up by the host (Geom::guard_par0); CFD_JACOBI_SUMS=0 keeps the
+    // reference's form everywhere
+    int sums = 0;
+    float plim = 0.0f, rlim = 0.0f;
+    if ((MODE == 0 || MODE == 1 || MODE == 2) && g.guard_par0 >= 0 && g.fastdiv == 1 &&
+        g.j0 == 0 && g.nyl == g.ny && g.dx_sq == g.dy_sq && g.r_dx_sq == g.r_dy_sq) {
+        const char *ue = getenv("CFD_JACOBI_SUMS");
+        int e2 = 0;
+        const float R = g.r_dx_sq;
+        if (!(ue && atoi(ue) == 0) && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
+            sums = 1;
+            plim = std::ldexp(1.0f, 124) / R;
+            rlim = std::ldexp(1.0f, 124);
+        }
+    }
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
     hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
-                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, spec_fold)
+                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, spec_fold, sums,  \
+                       plim, rlim, f.guard_slots)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);
     else if (g.fastdiv == 2)

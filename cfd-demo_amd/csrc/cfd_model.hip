@@ -1145,6 +1145,7 @@ struct cfd_model {
                 // launch runs kSpecT sweeps with every sweep's residual, a check
                 // finds the reference's early exit (model.rs:816), and the
                 // converged launch is re-run with exactly its sweeps
+                g.guard_par0 = 0;   // one guarded chain (k_jacobi_lds's SUMS form)
                 for (int it = 0; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
@@ -1155,6 +1156,7 @@ struct cfd_model {
                     it += T;
                     ++launches;
                 }
+                g.guard_par0 = -1;
                 if (iters > 0) launch_jacobi_redo(g, f, pass, lo_g, hi_g, stream);
             } else if (tmax <= 1) {
                 for (int it = 0; it < iters; ++it)
@@ -1164,7 +1166,7 @@ struct cfd_model {
             } else {
                 int it = 0;
                 last_persist_blocks = 0;
-                if (persist_env && !capturing && tmax == 8 && g.tb_kind == 5) {
+                if (persist_env && persist_req > 0 && !capturing && tmax == 8 && g.tb_kind == 5) {
                     // the leading run of full 8-sweep blocks as one persistent
                     // launch, the solve's last block (which publishes the
                     // residual) included when it is a full block too
@@ -1189,6 +1191,9 @@ struct cfd_model {
                         launches = nblk;
                     }
                 }
+                // the per-launch blocks form one guarded chain (the SUMS
+                // form's guard, k_jacobi_lds) from the first of them
+                g.guard_par0 = launches;
                 for (; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, tmax, iters, &T, &lo, &hi, &exch);
@@ -1197,6 +1202,7 @@ struct cfd_model {
                     it += T;
                     ++launches;
                 }
+                g.guard_par0 = -1;
             }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
         } else {
@@ -1422,12 +1428,16 @@ struct cfd_model {
 
     bool host_driven() const { return sharded() && params.tol_enabled; }
 
-    // Persistent fixed-count solve (k_jacobi_persist); CFD_PERSIST=0 opts out.
-    // Each launch gets a new flag epoch from the host (flags start at 0).
-    bool persist_env = [] {
+    // Persistent fixed-count solve (k_jacobi_persist); CFD_PERSIST=0 opts out
+    // everywhere.  Each launch gets a new flag epoch from the host (flags start
+    // at 0).  Single domain: opt-in (CFD_PERSIST=1) since r4 -- the per-launch
+    // march with the guarded SUMS form is faster there (profiles/r4); slabs
+    // keep the persistent runs between exchanges (CFD_PERSIST_SHARDED).
+    int persist_req = [] {
         const char *e = getenv("CFD_PERSIST");
-        return !(e && atoi(e) == 0);
+        return e ? atoi(e) : -1;
     }();
+    bool persist_env = persist_req != 0;
     // the solve's last (residual) block inside the persistent launch too;
     // CFD_PERSIST_RES=0 launches it on its own
     bool persist_res_env = [] {
@@ -1942,6 +1952,7 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // 7.3e11 vs 6.1e11 cell-updates/s at T = 8).  Single domain and slabs alike.
     g.tb_kind = g.fastdiv == 1 ? 5 : 4;
     g.pred_div = 2;
+    g.guard_par0 = -1;
     if (const char *e = getenv("CFD_PRED_DIV")) g.pred_div = std::min(std::max(atoi(e), 0), 2);
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
@@ -2104,7 +2115,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
     f.vis_slots = f.red_slots + (size_t)4 * kResSlots * kResStride;
-    f.persist = m->slots + (size_t)(kMaxSweeps + 8) * kResSlots * kResStride;
+    f.guard_slots = m->slots + (size_t)(kMaxSweeps + 8) * kResSlots * kResStride;
+    f.persist = m->slots + (size_t)(kMaxSweeps + 16) * kResSlots * kResStride;
 
     Ctl c0;
     std::memset(&c0, 0, sizeof(c0));
@@ -2783,9 +2795,11 @@ int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks) {
     if (!m || !blocks) return fail(CFD_EINVAL, "null argument");
     int rc = m->sync();
     if (rc) return rc;
-    uint32_t v = 0;
+    uint32_t v = 0, w = 0;
     HIP_TRY(hipMemcpy(&v, m->f.persist + 3, 4, hipMemcpyDeviceToHost));
-    *blocks = v;
+    HIP_TRY(hipMemcpy(&w, m->f.guard_slots + (size_t)kGuardSets * kResSlots * kResStride, 4,
+                      hipMemcpyDeviceToHost));
+    *blocks = (uint64_t)v + w;   // persistent blocks + per-launch blocks in the SUMS form
     return 0;
 }
 

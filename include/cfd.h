@@ -248,10 +248,12 @@ int cfd_get_persist_blocks(const cfd_model *m, int *blocks);
  * owner had not claimed them (k_jacobi_persist stealing; 0 when every owner
  * was resident), summed over the model's life.  Synchronises.  (new) */
 int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
-/* Persistent-solve blocks (per tile) run in the SUMS form -- (h + v) / dx^2
- * for h / dx^2 + v / dy^2, one instruction per column pair and sweep fewer,
- * taken only where a per-task guard proves it bitwise (k_jacobi_persist) --
- * summed over the model's life.  Synchronises.  (new; diagnostics) */
+/* 8-sweep blocks run in the SUMS form -- (h + v) / dx^2 for h / dx^2 +
+ * v / dy^2, one instruction per column pair and sweep fewer, taken only where
+ * a guard proves it bitwise: persistent-solve blocks per tile
+ * (k_jacobi_persist's per-task guard) plus per-launch blocks (k_jacobi_lds's
+ * chain guard) -- summed over the model's life.  Synchronises.  (new;
+ * diagnostics) */
 int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
 /* Tolerance-mode solves this model enqueued as one resident launch
  * (k_jacobi_resident, see cfd_get_jacobi_kernel kind 6); diagnostics. */

@@ -22,6 +22,14 @@ pytestmark = pytest.mark.gpu
 STATE = ("u", "v", "p", "u_star", "v_star", "p_prime", "rhs")
 
 
+@pytest.fixture(autouse=True)
+def _persistent_on(monkeypatch):
+    """Single-domain persistence is opt-in since r4 (the per-launch march
+    with the guarded SUMS form is the default there); these tests ask for it
+    unless they set CFD_PERSIST themselves."""
+    monkeypatch.setenv("CFD_PERSIST", "1")
+
+
 def pow2_grid(nx, ny, inv=512):
     """A cavity-type grid whose spacings are 1/inv (a power of two) whatever
     nx, ny are: the reciprocal-multiply division is proven exact there, so
@@ -343,8 +351,11 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     and the per-task guard falls back to the reference's form where a task
     reads a huge value: p' = 2^110 in one corner (the tiles there and those
     its values reach), rhs = 2^126 (> the 2^124 limit) in one patch (the
-    tiles that read it); distant tiles keep SUMS.  Every case bitwise vs
-    per-launch solves (CFD_PERSIST=0) and vs CFD_JACOBI_SUMS=0."""
+    tiles that read it); distant tiles keep SUMS.  The per-launch march's
+    chain guard (k_jacobi_lds, r4: global maxima, the solve's first launch
+    exact) takes SUMS on launches 1..24 of the plain case and none where a
+    huge value sits anywhere.  Every case bitwise vs per-launch solves in the
+    reference's form (CFD_PERSIST=0, CFD_JACOBI_SUMS=0)."""
     import cfdamd
     grid = cfdamd.cavity_grid(1024)
     params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
@@ -361,8 +372,11 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     rhs_huge[500:520, 300:340] = np.float32(2.0 ** 126)
     cases = {"plain": {}, "huge_pp": {"p_prime": pp_huge.ravel()},
              "huge_rhs": {"rhs": rhs_huge.ravel()}}
-    envs = {"per_launch": {"CFD_PERSIST": "0"}, "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0"},
+    envs = {"per_launch": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "0"},
+            "per_launch_sums": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "1"},
+            "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0"},
             "sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "1"}}
+    per_launch_sums = {}
     sums = {}
     for name, inject in cases.items():
         out = {}
@@ -379,7 +393,12 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
         for key, (pp, _, _) in out.items():
             assert_bitwise(f"sums {name} [{key}]:p_prime", pp, out["per_launch"][0])
         assert out["sums"][1] == 25 and out["no_sums"][2] == 0, (out["sums"][1:], out["no_sums"][1:])
+        assert out["per_launch"][1:] == (0, 0), out["per_launch"][1:]
         sums[name] = out["sums"][2]
+        per_launch_sums[name] = out["per_launch_sums"][2]
+    # per-launch chain (k_jacobi_lds, global guard): launches 1..24 of the 25
+    # in the SUMS form; a huge p' or rhs anywhere keeps every launch exact
+    assert per_launch_sums == {"plain": 24, "huge_pp": 0, "huge_rhs": 0}, per_launch_sums
     # plain: the owned tiles' blocks 2..24 (blocks 0 and 1 measure the inputs)
     assert sums["plain"] > 0, sums
     assert 0 < sums["huge_pp"] < sums["plain"] and 0 < sums["huge_rhs"] < sums["plain"], sums
