@@ -117,9 +117,10 @@ constexpr int ring_depth(int T, int PD, int G) {
 // overflow included; a subnormal h + v is exact).  k_jacobi_persist proves
 // that bound per task before it picks SUMS (its guard); otherwise, and for
 // every other launch, the reference's form runs.
-// GRD (r4, per-launch solves on a single domain, k_jacobi_lds): 1 = a launch
-// of a guarded chain, tracks max |p'| of what it stores (omax, the next
-// launch's guard); 2 = the chain's first launch, also max |rhs| (rmax).
+// GRD (r4, per-launch solves on a single domain, k_jacobi_lds): 2 = the
+// solve's first launch, tracks max |p'| of every input it loads (imax) and
+// max |rhs| (rmax) for the whole-solve SUMS guard; 1 = a later launch of the
+// solve (no tracking; lds_block decides its form from those two maxima).
 template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1 || MODE == 5, SPEC = MODE == 2, REDO = MODE == 3;
@@ -136,7 +137,7 @@ struct LdsMarch {
 #define CFD_PROBE_NOTRACK 0   // (diagnostic builds: no guard tracking)
 #endif
     static constexpr bool TRACK_IN = (PERSIST && !SUMS && !CFD_PROBE_NOTRACK) || GRD == 2;
-    static constexpr bool TRACK_OUT = (PERSIST && !CFD_PROBE_NOTRACK) || GRD > 0;
+    static constexpr bool TRACK_OUT = PERSIST && !CFD_PROBE_NOTRACK;
     static_assert(!SUMS || FAST == 1, "SUMS: reciprocal multiply");
     static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
     static constexpr int PST_AUX = PERSIST ? 16 : CFD_LDS_ST_AUX;
@@ -464,6 +465,22 @@ struct LdsMarch {
 // trk (persistent blocks): per wave, trk[3 w .. 3 w + 2] = max |p'| of the
 // rows it stored, of the p' rows it loaded and of the rhs rows it used (the
 // last two only in the reference's form; 0 where not tracked or no rows).
+// The whole-solve SUMS guard of a per-launch single-domain solve.  M0 =
+// max |p'| the solve's first launch read (every cell of the source buffer;
+// the other buffer holds only values the solve itself stores), Rm = max
+// |rhs|.  A sweep moves max |p'| by at most 0.1875 Rm / R (|pu| <= M +
+// Rm / (4R), p_new = 0.75 pu + 0.25 p), so every value of the solve's
+// K = jacobi_iters sweeps stays below M0 + K 0.1875 Rm / R (rounding: a
+// factor 1 + 2^-12 at most over 512 sweeps); below plim = 2^124 / R every
+// h R, v R is < 2^126, the form's exactness bound.  NaN: max ignores it
+// and it propagates as the same operand in both forms; +-Inf fails.
+__device__ __forceinline__ bool sums_guard(float m0, float rm, float plim, float rlim, const Geom &g) {
+    // 0.1875 K Rm / R = 0.1875 K Rm dx^2 (FAST == 1 with R a power of two
+    // makes dx^2 exactly 1 / R)
+    const float drift = 0.1875f * (float)g.jacobi_iters * rm * g.dx_sq;
+    return m0 < 0.5f * plim && rm < rlim && drift < 0.5f * plim;
+}
+
 template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
 __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           float *__restrict__ pb, const float *__restrict__ rhs,
@@ -582,14 +599,14 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         wx.template run<MX::kCol>();
     else
         wx.template run<0>();
-    if constexpr (GRD > 0) {
-        // the guard chain: this launch's stored maximum (and the solve's
-        // rhs maximum), one spread slot per wave
-        const float o = wave_max(out_lane ? wx.omax : 0.0f);
-        if (lane == 0) publish_max(gset, bid * kLdsWaves + wave, o);
-        if constexpr (GRD == 2) {
-            const float rm = wave_max(wx.rmax);
-            if (lane == 0) publish_max(grhs, bid * kLdsWaves + wave, rm);
+    if constexpr (GRD == 2) {
+        // the whole-solve guard's inputs: max |p'| of what this first launch
+        // read and max |rhs|, one spread slot per wave
+        const float im = wave_max(wx.imax);
+        const float rm = wave_max(wx.rmax);
+        if (lane == 0) {
+            publish_max(gset, bid * kLdsWaves + wave, im);
+            publish_max(grhs, bid * kLdsWaves + wave, rm);
         }
     }
     if (M::PERSIST && trk) {
@@ -627,12 +644,12 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     };
     if constexpr (FAST == 1 && GRD == 1 && !SUMS && !M::PERSIST) {
         if (gprev) {
-            // the chain guard's two maxima, loaded while the prefetch is in
-            // flight (one global round trip for both)
+            // the whole-solve guard's two maxima, loaded while the prefetch is
+            // in flight (one global round trip for both)
             const int gl = lane & (kResSlots - 1);
             const float pin = wave_max(__uint_as_float(gprev[gl * kResStride]));
             const float rin = wave_max(__uint_as_float(grhs[gl * kResStride]));
-            if (pin < plim && rin < rlim) {
+            if (sums_guard(pin, rin, plim, rlim, g)) {
                 if (bid == 0 && threadIdx.x == 0)   // diagnostics: launches in the SUMS form
                     atomicAdd(grhs + (size_t)kResSlots * kResStride, 1u);   // set kGuardSets
                 LdsMarch<T, FAST, MODE, true, GRD> w1(w);
@@ -756,35 +773,29 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         const int gp = par - g.guard_par0;
         if (sums && g.guard_par0 >= 0 && gp >= 0) {
             constexpr size_t kSet = (size_t)kResSlots * kResStride;
-            uint32_t *own = gslots + (size_t)(gp & 3) * kSet;
-            if (blockIdx.x == 0 && threadIdx.x < kResSlots)   // the set launch g+2 will fill
-                gslots[(size_t)((gp + 2) & 3) * kSet + threadIdx.x * kResStride] = 0u;
+            uint32_t *const gin = gslots, *const grh = gslots + 4 * kSet;   // sets 0 and 4
             const int bid = xcd_block(g);
             if (gp == 0) {
                 lds_block<T, FAST, MODE, false, 2>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
                                                    nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
-                                                   nullptr, own, gslots + 4 * kSet);
+                                                   nullptr, gin, grh);
             } else if constexpr (MODE != 2) {
                 // the guard is decided inside (lds_block: its loads overlap the prefetch)
                 lds_block<T, FAST, MODE, false, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
                                                    nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
-                                                   nullptr, own, gslots + 4 * kSet,
-                                                   gslots + (size_t)((gp - 1) & 3) * kSet, plim, rlim);
+                                                   nullptr, nullptr, grh, gin, plim, rlim);
             } else {
                 // the speculative launch (5 waves per SIMD: 96 registers) decides
                 // first: both forms' state live across the decision spills there
-                const float pin = read_max(gslots + (size_t)((gp - 1) & 3) * kSet, 0u);
-                const float rin = read_max(gslots + 4 * kSet, 0u);
-                if (pin < plim && rin < rlim) {
+                if (sums_guard(read_max(gin, 0u), read_max(grh, 0u), plim, rlim, g)) {
                     if (blockIdx.x == 0 && threadIdx.x == 0)   // diagnostics: SUMS launches
                         atomicAdd(gslots + (size_t)kGuardSets * kSet, 1u);
-                    lds_block<T, FAST, MODE, true, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo,
-                                                      out_hi, nwc, nseg, wlo, whi, lds, nst, bid,
-                                                      spec_fold, nullptr, own);
+                    lds_block<T, FAST, MODE, true>(g, pa, pb, rhs, ctl, res_slots, par, out_lo,
+                                                   out_hi, nwc, nseg, wlo, whi, lds, nst, bid,
+                                                   spec_fold);
                 } else {
-                    lds_block<T, FAST, MODE, false, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo,
-                                                       out_hi, nwc, nseg, wlo, whi, lds, nst, bid,
-                                                       spec_fold, nullptr, own);
+                    lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc,
+                                             nseg, wlo, whi, lds, nst, bid, spec_fold);
                 }
             }
             if (M::SPEC && spec_fold) spec_check_tail<T>(g, ctl, res_slots, it, par);
@@ -1216,8 +1227,10 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int spec_fold = MODE == 2 && spec_fold_on() ? 1 : 0;
     // the guarded SUMS form (k_jacobi_lds): reciprocal multiply, dx^2 ==
     // dy^2 with a power-of-two reciprocal R >= 1, single domain, a chain set
-    // up by the host (Geom::guard_par0); CFD_JACOBI_SUMS=0 keeps the
-    // reference's form everywhere
+    // up by the host (Geom::guard_par0).  Opt-in here (CFD_JACOBI_SUMS=1):
+    // with the guard in, the per-launch march measured no faster (4096^2
+    // 5.09 vs 5.03 us per sweep, C3 11.46 vs 11.19 ms, ab_*_r4p.log; the
+    // unguarded probe 4.92 vs 5.09, ab_4096_r4m.log)
     int sums = 0;
     float plim = 0.0f, rlim = 0.0f;
     if ((MODE == 0 || MODE == 1 || MODE == 2) && g.guard_par0 >= 0 && g.fastdiv == 1 &&
@@ -1225,7 +1238,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
         const char *ue = getenv("CFD_JACOBI_SUMS");
         int e2 = 0;
         const float R = g.r_dx_sq;
-        if (!(ue && atoi(ue) == 0) && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
+        if (ue && atoi(ue) == 1 && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
             sums = 1;
             plim = std::ldexp(1.0f, 124) / R;
             rlim = std::ldexp(1.0f, 124);

@@ -19,6 +19,10 @@ step() {  # step <name> <seconds> <cmd...>
 }
 B="python3 bench.py --no-cpu-baseline --no-parity --no-control --no-so --no-parity-mode --no-reference-default"
 P="--develop 30 --warmup 0 --steps 2"
+if [ "${SUITE:-0}" = 1 ]; then
+  step suite 1000 python -u -m pytest tests -x -v -m gpu --timeout 400 --timeout-method thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+fi
 if [ "${BENCH:-1}" = 1 ]; then
   # the driver's command, unprofiled: the line whose kernel time the stats must agree with
   step bench_default 600 python3 bench.py
@@ -40,6 +44,8 @@ if [ "${PMC:-1}" = 1 ]; then
   # single-domain proxies with their 32 + 32 ghost rows, at the global grids'
   # power-of-two spacing: same kernel, same geometry (pad keyed on owned rows)
   export TB_WARMUP=30   # rocprofv3 runs the program itself (no env hop)
+  # a rank slab runs the persistent launch between its exchanges: profile that
+  export CFD_PERSIST=1
   for S in 8192x2112@4096:8192x2048 16384x1088@8192:16384x1024; do
     SH=${S%%:*}; WL=${S##*:}
     C="TB_WARMUP=30 python3 tools/tb_one.py $SH 2"
@@ -49,10 +55,11 @@ if [ "${PMC:-1}" = 1 ]; then
     step pmc_valu_$WL 150 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE -d $D -o valu_$WL --output-format csv -- python3 tools/tb_one.py $SH 2
     python3 tools/pmc_valu.py $D/valu_${WL}_counter_collection.csv --workload $WL --command "$C" --persist-blocks 25 --note "single-domain proxy $SH of the rank slab" -o $D/pmc_valu_${WL}.json
   done
+  unset CFD_PERSIST TB_WARMUP
 fi
 if [ "${SLABS:-0}" = 1 ]; then
   for shape in 4096 8192x2112@4096 16384x1088@8192; do
-    step slab_shape_$shape 420 env AB_CMD="tb_one.py $shape 5" TB_WARMUP=300 python3 -u tools/ab_env.py "" "CFD_LDS_PAD=0" "CFD_LDS_PAD=24576" "CFD_PERSIST=0"
+    step slab_shape_$shape 420 env AB_CMD="tb_one.py $shape 5" TB_WARMUP=300 python3 -u tools/ab_env.py "" "CFD_LDS_PAD=0" "CFD_LDS_PAD=24576" "CFD_PERSIST=1"
   done
 fi
 if [ "${REHEARSE:-0}" = 1 ]; then
