@@ -759,7 +759,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         if (nst <= 0) return;
         par = ctl->spec_launch;   // re-run that launch: same source, same destination
     }
-    if constexpr (FAST == 1 && (MODE == 0 || MODE == 1 || MODE == 2)) {
+    if constexpr (FAST == 1 && (MODE == 0 || MODE == 1)) {
         // The SUMS form on a guarded chain of launches (single domain; sums:
         // the grid allows the form at all, see LdsMarch).  Launch g of the
         // chain reads exactly what launch g-1 stored (every p' cell, boundary
@@ -779,26 +779,12 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
                 lds_block<T, FAST, MODE, false, 2>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
                                                    nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
                                                    nullptr, gin, grh);
-            } else if constexpr (MODE != 2) {
+            } else {
                 // the guard is decided inside (lds_block: its loads overlap the prefetch)
                 lds_block<T, FAST, MODE, false, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
                                                    nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
                                                    nullptr, nullptr, grh, gin, plim, rlim);
-            } else {
-                // the speculative launch (5 waves per SIMD: 96 registers) decides
-                // first: both forms' state live across the decision spills there
-                if (sums_guard(read_max(gin, 0u), read_max(grh, 0u), plim, rlim, g)) {
-                    if (blockIdx.x == 0 && threadIdx.x == 0)   // diagnostics: SUMS launches
-                        atomicAdd(gslots + (size_t)kGuardSets * kSet, 1u);
-                    lds_block<T, FAST, MODE, true>(g, pa, pb, rhs, ctl, res_slots, par, out_lo,
-                                                   out_hi, nwc, nseg, wlo, whi, lds, nst, bid,
-                                                   spec_fold);
-                } else {
-                    lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc,
-                                             nseg, wlo, whi, lds, nst, bid, spec_fold);
-                }
             }
-            if (M::SPEC && spec_fold) spec_check_tail<T>(g, ctl, res_slots, it, par);
             return;
         }
     }
@@ -1233,7 +1219,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     // unguarded probe 4.92 vs 5.09, ab_4096_r4m.log)
     int sums = 0;
     float plim = 0.0f, rlim = 0.0f;
-    if ((MODE == 0 || MODE == 1 || MODE == 2) && g.guard_par0 >= 0 && g.fastdiv == 1 &&
+    if ((MODE == 0 || MODE == 1) && g.guard_par0 >= 0 && g.fastdiv == 1 &&
         g.j0 == 0 && g.nyl == g.ny && g.dx_sq == g.dy_sq && g.r_dx_sq == g.r_dy_sq) {
         const char *ue = getenv("CFD_JACOBI_SUMS");
         int e2 = 0;
