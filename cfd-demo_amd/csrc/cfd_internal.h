@@ -42,9 +42,10 @@ constexpr int kResStride = 16;
 // block
 constexpr int kPersistFlagStride = 16;
 // head lines: 0 = the persistent solve's words ([1] abort, [2] steals, [3]
-// SUMS blocks); 2 = the resident solve's barrier counter, 4 = its exit ticket
-// (cfd_jacobi_resident.hip; own 128-B lines)
-constexpr int kPersistHeadLines = 5;
+// SUMS blocks); 2 = the resident solve's top barrier counter, 4 = its exit
+// ticket, 5-12 its group counters, 13-20 its group generations
+// (cfd_jacobi_resident.hip)
+constexpr int kPersistHeadLines = 21;
 // flag = epoch << kPersistBlockBits | blocks done: room for every block of the
 // longest solve (kMaxSweeps / 8 = 512), epochs below 2^(32 - bits)
 constexpr int kPersistBlockBits = 10;

@@ -42,9 +42,12 @@
 // them (vmcnt(0)) before the workgroup barrier, then one lane adds to the
 // barrier counter (agent scope); the waiting lane polls it (relaxed agent
 // loads, s_sleep), then one agent acquire + vmcnt(0) + the workgroup barrier
-// before any p' load.  The counter and an exit ticket live in Fields::persist's
-// head lines 2 and 4; the workgroup that draws the last exit ticket zeroes
-// both, so every launch starts from 0.
+// before any p' load.  The counters and an exit ticket live in
+// Fields::persist's head lines (2: top / single counter, 4: exit ticket, 5-12:
+// group counters, 13-20: group generations); the workgroup that draws the
+// last exit ticket zeroes them, so every launch starts from 0.
+#include <cstring>
+
 #include "cfd_device.h"
 
 namespace cfd {
@@ -58,7 +61,7 @@ constexpr int kResMaxT = 8;
 template <int FAST, int WAVES, int ROWS>
 __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
     Geom g, Fields f, int pass, int iters, int T, int BR, int BC, int tiles_x, int ntiles,
-    int res_hi, uint32_t deadline, int late, int fin, int check_break) {
+    int res_hi, uint32_t deadline, int late, int fin, int check_break, int xbar) {
     constexpr int kResWaves = WAVES;
     extern __shared__ float lds_dyn[];
     __shared__ float red_s[kResWaves][kResMaxT];
@@ -260,18 +263,43 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t want = (uint32_t)G * (uint32_t)(k + 1);
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             int fail = 0;
-            for (;;) {
-                if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-                if (__hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-                    __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)deadline) {
-                    fail = 1;
-                    break;
+            // wait until *w >= want (relaxed agent polls, bounded)
+            auto wait_ge = [&](uint32_t *w, uint32_t want) {
+                for (;;) {
+                    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return;
+                    if (__hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                        __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)deadline) {
+                        fail = 1;
+                        return;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                __builtin_amdgcn_s_sleep(1);
+            };
+            if (!xbar) {
+                // one counter, G pollers
+                __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wait_ge(bar, (uint32_t)G * (uint32_t)(k + 1));
+            } else {
+                // two levels (MI355X_MICROARCH.md barrier-xcd): workgroup w
+                // arrives on group counter w % 8 (round-robin dispatch puts a
+                // group on one XCD: speed only, never correctness); the
+                // group's last arriver (told by its returning add) arrives on
+                // the top counter, waits for all groups and raises the group's
+                // generation word, which the group's other workgroups poll
+                const int grp = wg & 7, ngrp = G < 8 ? G : 8;
+                const uint32_t gsize = (uint32_t)(G / 8 + (grp < G % 8 ? 1 : 0));
+                uint32_t *gc = persist + (5 + grp) * kPersistFlagStride;
+                uint32_t *gg = persist + (13 + grp) * kPersistFlagStride;
+                const uint32_t v = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v + 1u == gsize * (uint32_t)(k + 1)) {
+                    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    wait_ge(bar, (uint32_t)ngrp * (uint32_t)(k + 1));
+                    __hip_atomic_store(gg, (uint32_t)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    wait_ge(gg, (uint32_t)(k + 1));
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -318,6 +346,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
             __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)G - 1u;
         if (lastwg) {
             __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int q = 0; q < 8; ++q) {
+                __hip_atomic_store(persist + (5 + q) * kPersistFlagStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(persist + (13 + q) * kPersistFlagStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
             __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (fin) {
                 ctl->spec_launches = blocks;   // every workgroup ran the same blocks
@@ -415,12 +449,15 @@ bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters,
     const uint32_t deadline = (uint32_t)std::min(4.0e9, dl_us * 100.0);
     const char *le = getenv("CFD_PERSIST_LATE");
     const int late = le ? std::max(0, atoi(le)) : 0;
+    // the grid barrier: two-level (default) or one counter (CFD_RESIDENT_BAR=flat)
+    const char *be = getenv("CFD_RESIDENT_BAR");
+    const int xbar = be && strcmp(be, "flat") == 0 ? 0 : 1;
     const char *re = getenv("CFD_RESIDENT_ROWS");
     const int rows = re ? atoi(re) : 2;
 #define CFD_RES_LAUNCH(FASTV, WV, RW)                                                              \
     hipLaunchKernelGGL((k_jacobi_resident<FASTV, WV, RW>), dim3(p.G), dim3(WV * 64), p.lds, s, g, \
                        f, pass, iters, T, p.BR, p.BC, p.tiles_x, p.ntiles,                        \
-                       resident_simd_end(g.nx), deadline, late, fin, check_break)
+                       resident_simd_end(g.nx), deadline, late, fin, check_break, xbar)
 #define CFD_RES_WAVES(FASTV)                \
     if (resident_waves() == 16)             \
         CFD_RES_LAUNCH(FASTV, 16, 2);       \
