@@ -192,11 +192,14 @@ def reference_default_leg(args, cfdamd, device, develop=200, steps=20, cpu_steps
         el = time.perf_counter() - t0
         sweeps = m.get_residuals().jacobi_sweeps_total - s0
         kc = m.kernel_config
+        kname = m.jacobi_kernel["name"]
+        division = ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
+                    "FMA-corrected (proven exact, 2^32 inputs)"][kc["fastdiv"]]
+        if kname == "k_jacobi_resident<3>":   # the resident solve's guarded form
+            division = "FMA-corrected for |x| >= 2^-96, IEEE below (proven exact, 2^32 inputs)"
         e = {"steps": steps, "ms_per_step": 1e3 * el / steps, "sweeps_per_step": sweeps / steps,
              "cell_updates_per_s": grid.nx * grid.ny * sweeps / el,
-             "kernel": m.jacobi_kernel["name"],
-             "division": ["IEEE", "reciprocal multiply (proven exact, 2^32 inputs)",
-                          "FMA-corrected (proven exact, 2^32 inputs)"][kc["fastdiv"]]}
+             "kernel": kname, "division": division}
         state = m.get_state()
         if not args.no_parity:
             o, orc = oracle_from_state(0, 0, 0, 0, state, cpu_threads(), grid=grid, params=params)

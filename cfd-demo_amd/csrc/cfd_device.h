@@ -78,6 +78,11 @@ __device__ __forceinline__ float from_right(float x) {
 // x / c with the reference's IEEE rounding.  FAST 1 and 2 are used only for
 // divisors whose result equals IEEE `/` for every one of the 2^32 inputs,
 // proven on the device at model creation (verify_division, cfd_model.hip).
+// FAST 3 (r4): the FMA-corrected form for |x| >= 2^-96 and IEEE `/` below
+// (where the correction's residual underflows: every mismatch of form 2 on
+// the reference's default-grid divisors lies at |x| < 2^-104), proven for all
+// 2^32 inputs per divisor like the others; NaN takes the IEEE branch.
+constexpr float kDivGuardMin = 0x1p-96f;
 template <int FAST>
 __device__ __forceinline__ float fdiv(float x, float c, float r) {
     if (FAST == 1) return x * r;
@@ -85,6 +90,13 @@ __device__ __forceinline__ float fdiv(float x, float c, float r) {
         const float q0 = x * r;
         const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
         return __builtin_isfinite(q0) ? q : q0;
+    }
+    if (FAST == 3) {
+        if (__builtin_expect(__builtin_fabsf(x) >= kDivGuardMin, 1)) {
+            const float q0 = x * r;
+            const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
+            return __builtin_isfinite(q0) ? q : q0;
+        }
     }
     return x / c;
 }

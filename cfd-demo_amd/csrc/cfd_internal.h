@@ -123,6 +123,8 @@ struct Geom {
     int32_t pred_div;     // predictors + divergence: 2: one row march (k_predict_march, both
                           // schemes), 1: fused 2-row tile (k_predict_div, first order),
                           // 0: separate launches; where the fused forms apply
+    int32_t res_div;      // r4: the resident solve's division mode: fastdiv, or 3 (FMA-corrected
+                          // above 2^-96, IEEE below; proven like the others) where fastdiv is 0
     int32_t guard_par0;   // r4: the solve's first k_jacobi_lds launch index of a guarded
                           // chain (the SUMS form's guard, Fields::guard_slots); -1: none
 };

@@ -407,8 +407,9 @@ bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
             if (&cd != &cand[0]) break;
         }
         const int lds = resident_lds_bytes(BR, BC, T);
-        const int occ = g.fastdiv == 1   ? resident_blocks_per_cu<1>(lds)
-                        : g.fastdiv == 2 ? resident_blocks_per_cu<2>(lds)
+        const int occ = g.res_div == 1   ? resident_blocks_per_cu<1>(lds)
+                        : g.res_div == 2 ? resident_blocks_per_cu<2>(lds)
+                        : g.res_div == 3 ? resident_blocks_per_cu<3>(lds)
                                          : resident_blocks_per_cu<0>(lds);
         if (occ < 2) continue;
         const int tx = cdiv(g.nx, BC), ty = cdiv(g.ny, BR);
@@ -467,10 +468,12 @@ bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters,
         CFD_RES_LAUNCH(FASTV, 8, 4);        \
     else                                    \
         CFD_RES_LAUNCH(FASTV, 8, 2);
-    if (g.fastdiv == 1) {
+    if (g.res_div == 1) {
         CFD_RES_WAVES(1)
-    } else if (g.fastdiv == 2) {
+    } else if (g.res_div == 2) {
         CFD_RES_WAVES(2)
+    } else if (g.res_div == 3) {
+        CFD_RES_WAVES(3)
     } else {
         CFD_RES_WAVES(0)
     }

@@ -21,24 +21,28 @@ __global__ __launch_bounds__(kBlock) void k_verify_division(float c, float r,
                                                             unsigned long long *counts) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
-    uint32_t bad1 = 0, bad2 = 0;
+    uint32_t bad1 = 0, bad2 = 0, bad3 = 0;
     for (uint64_t k = tid; k < (1ull << 32); k += stride) {
         const float x = __uint_as_float((uint32_t)k);
         const float ref = x / c;
         const float m1 = fdiv<1>(x, c, r);
         const float m2 = fdiv<2>(x, c, r);
+        const float m3 = fdiv<3>(x, c, r);
         const bool rn = ref != ref;
         bad1 += (rn ? (m1 == m1) : (__float_as_uint(m1) != __float_as_uint(ref))) ? 1u : 0u;
         bad2 += (rn ? (m2 == m2) : (__float_as_uint(m2) != __float_as_uint(ref))) ? 1u : 0u;
+        bad3 += (rn ? (m3 == m3) : (__float_as_uint(m3) != __float_as_uint(ref))) ? 1u : 0u;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         bad1 += __shfl_xor(bad1, o, 64);
         bad2 += __shfl_xor(bad2, o, 64);
+        bad3 += __shfl_xor(bad3, o, 64);
     }
     if ((threadIdx.x & 63) == 0) {
         if (bad1) atomicAdd(&counts[0], (unsigned long long)bad1);
         if (bad2) atomicAdd(&counts[1], (unsigned long long)bad2);
+        if (bad3) atomicAdd(&counts[2], (unsigned long long)bad3);
     }
 }
 

@@ -1853,15 +1853,15 @@ int division_ok_mask(hipStream_t s, float c, float r, int *mask) {
                 return 0;
             }
     }
-    unsigned long long *d = nullptr, h[2] = {0, 0};
-    HIP_TRY(hipMalloc((void **)&d, 16));
-    HIP_TRY(hipMemsetAsync(d, 0, 16, s));
+    unsigned long long *d = nullptr, h[3] = {0, 0, 0};
+    HIP_TRY(hipMalloc((void **)&d, 24));
+    HIP_TRY(hipMemsetAsync(d, 0, 24, s));
     launch_verify_division(c, r, d, s);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h, d, 24, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipFree(d));
-    *mask = (h[0] == 0 ? 1 : 0) | (h[1] == 0 ? 2 : 0);
+    *mask = (h[0] == 0 ? 1 : 0) | (h[1] == 0 ? 2 : 0) | (h[2] == 0 ? 4 : 0);
     std::lock_guard<std::mutex> lk(g_div_mu);
     g_div_cache.emplace_back(bits, *mask);
     return 0;
@@ -1869,6 +1869,7 @@ int division_ok_mask(hipStream_t s, float c, float r, int *mask) {
 
 int choose_division(hipStream_t s, Geom &g) {
     g.fastdiv = 0;
+    g.res_div = 0;
     const char *env = getenv("CFD_FASTDIV");
     if (env && atoi(env) == 0) return 0;
     int m1, m2, m3;
@@ -1880,6 +1881,8 @@ int choose_division(hipStream_t s, Geom &g) {
     const int all = m1 & m2 & m3;
     g.fastdiv = (all & 1) ? 1 : (all & 2) ? 2 : 0;
     if (env && atoi(env) == 2 && (all & 2)) g.fastdiv = 2;   // test hook: prefer mode 2
+    // the resident solve also has the guarded FMA form (3)
+    g.res_div = g.fastdiv != 0 ? g.fastdiv : (all & 4) ? 3 : 0;
     return 0;
 }
 
@@ -2746,7 +2749,7 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
     if (name && name_len) {
         char buf[96];
         if (resident)
-            snprintf(buf, sizeof buf, "k_jacobi_resident<%d>", m->g.fastdiv);
+            snprintf(buf, sizeof buf, "k_jacobi_resident<%d>", m->g.res_div);
         else if (spec)
             snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, 2>", T, m->g.fastdiv);
         else if (k == 0)

@@ -286,3 +286,41 @@ def test_resident_two_models_interleaved(monkeypatch):
     finally:
         for m in ms:
             m.close()
+
+
+def test_resident_guarded_fma_division_tiny_values(monkeypatch):
+    """On the reference's default grid no divisor has an exact reciprocal or
+    FMA-corrected form for all inputs, but form 3 -- FMA-corrected for
+    |x| >= 2^-96, IEEE `/` below, proven on the device for all 2^32 inputs --
+    holds, and the resident solve uses it.  p' scaled to 1e-33 in half the
+    domain (sums far below the threshold: the IEEE branch, in waves mixed with
+    the FMA branch) and a developed state elsewhere: three steps bitwise
+    against the oracle, sweep counts included."""
+    import cfdamd
+    from oracle import OracleModel
+    monkeypatch.setenv("CFD_RESIDENT", "1")
+    grid = cfdamd.default_grid()
+    m = cfdamd.Model(grid, cfdamd.SimulationParams(), device=0)
+    try:
+        assert m.jacobi_kernel["name"] == "k_jacobi_resident<3>", m.jacobi_kernel
+        m.update_n(6)
+        st = m.get_state()
+        pp = st["p_prime"].copy().reshape(grid.ny, grid.nx)
+        pp[:, : grid.nx // 2] *= np.float32(1e-33)
+        st["p_prime"] = pp.ravel()
+        m.set_state(**st)
+        c = grid.obstacle
+        o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly, cylinder=(c.center_x, c.center_y, c.radius))
+        for k in STATE:
+            o.field(k)[:] = st[k]
+        sc = o.scalars()
+        sc.step, sc.time, sc.dt = st["simulation_step"], st["simulation_time"], st["dt"]
+        sc.jacobi_sweeps_total = st["jacobi_sweeps_total"]
+        o.set_scalars(sc)
+        for k in range(3):
+            m.update()
+            o.update()
+            _compare(f"tiny p' step {k + 1}", m, o)
+        assert m.resident_solves >= 3
+    finally:
+        m.close()
