@@ -1881,8 +1881,12 @@ int choose_division(hipStream_t s, Geom &g) {
     const int all = m1 & m2 & m3;
     g.fastdiv = (all & 1) ? 1 : (all & 2) ? 2 : 0;
     if (env && atoi(env) == 2 && (all & 2)) g.fastdiv = 2;   // test hook: prefer mode 2
-    // the resident solve also has the guarded FMA form (3)
-    g.res_div = g.fastdiv != 0 ? g.fastdiv : (all & 4) ? 3 : 0;
+    // the resident solve also has the guarded FMA form (3), opt-in
+    // (CFD_RESIDENT_DIV=3): its per-division branch measured slower than
+    // IEEE division on the reference default (3.87 vs 3.57 ms per step,
+    // profiles/r4/ab_refdef_r4t.log)
+    const char *rd = getenv("CFD_RESIDENT_DIV");
+    g.res_div = g.fastdiv != 0 ? g.fastdiv : (rd && atoi(rd) == 3 && (all & 4)) ? 3 : 0;
     return 0;
 }
 
