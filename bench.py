@@ -816,7 +816,12 @@ def main():
                 out["cpu_baseline_multicore"] = cpu_baseline(
                     nx, ny, args.iters, args.re, args.cpu_budget / 2, state, threads=nt,
                     max_steps=9)
-        print(json.dumps(out), flush=True)
+        # ONE write for the whole line: other ranks share this stdout under an
+        # external launcher, and a line split over several writes can be cut
+        sys.stdout.flush()
+        data = (json.dumps(out) + "\n").encode()
+        while data:
+            data = data[os.write(1, data):]
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

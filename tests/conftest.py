@@ -8,7 +8,19 @@ for p in (ROOT, os.path.join(ROOT, "cfd-demo_amd"), os.path.join(ROOT, "oracle")
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# Files whose tests start several processes on the GPU (RCCL over loopback,
+# bench.py self-launch).  They run after every single-process parity file, so
+# a harness fault there cannot hide the oracle checks behind it under -x (r4).
+MULTI_PROCESS_FILES = ("test_gpu_rccl.py",)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests proper")
     config.addinivalue_line("markers", "slow: long-running")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    late = [it for it in items if os.path.basename(str(it.fspath)) in MULTI_PROCESS_FILES]
+    if late:
+        early = [it for it in items if os.path.basename(str(it.fspath)) not in MULTI_PROCESS_FILES]
+        items[:] = early + late

@@ -9,7 +9,6 @@ model bit for bit, in the bench's fixed-count mode (deep halos, overlapped
 band exchange, persistent runs between exchanges -- since r4 with the ranks'
 kernels sharing the GPU) and in the reference's tolerance mode (lagged
 convergence)."""
-import json
 import os
 import subprocess
 import sys
@@ -18,12 +17,14 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from jsonl import records  # noqa: E402  (tolerant: several objects per line)
 
 
 def test_rccl_two_ranks_bitwise_single_domain():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_loopback.py"),
                         "--n", "2", "--steps", "4"], capture_output=True, text=True, timeout=300)
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = records(r.stdout)
     assert r.returncode == 0 and len(lines) == 2, (r.stdout[-2000:], r.stderr[-3000:])
     assert all(x["bitwise_equal_single_domain"] for x in lines), lines
 
@@ -34,7 +35,7 @@ def test_rccl_two_ranks_solvers_bitwise_single_domain():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_loopback.py"),
                         "--n", "2", "--steps", "3", "--mode", "solvers"], capture_output=True,
                        text=True, timeout=300)
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = records(r.stdout)
     assert r.returncode == 0 and len(lines) == 4, (r.stdout[-2000:], r.stderr[-3000:])
     assert all(x["bitwise_equal_single_domain"] for x in lines), lines
 
@@ -85,7 +86,7 @@ def test_bench_self_launch_two_ranks_loopback():
                         "--steps", "3", "--warmup", "1", "--develop", "10", "--nx", "1024",
                         "--ny", "512", "--iters", "64"], env=env, capture_output=True,
                        text=True, timeout=300)
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.lstrip().startswith("{")]
+    lines = records(r.stdout)
     assert r.returncode == 0 and len(lines) == 1, (r.stdout[-2000:], r.stderr[-3000:])
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2, lines[0]
     assert lines[0]["launcher"] == "bench.py" and len(lines[0]["rank_ms_per_step"]) == 2
@@ -114,7 +115,7 @@ def test_rccl_developed_full_size_slabs_bitwise(n, nx, ny):
                         "--n", str(n), "--nx", str(nx), "--ny", str(ny), "--steps", "2",
                         "--develop", "400", "--mode", "developed", "--timeout", "400"],
                        capture_output=True, text=True, timeout=480)
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    lines = records(r.stdout)
     assert r.returncode == 0 and len(lines) == n, (r.stdout[-2000:], r.stderr[-3000:])
     for x in lines:
         assert x["bitwise_equal_single_domain"], x

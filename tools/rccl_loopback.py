@@ -15,18 +15,40 @@ compared bit for bit with a single-domain model of the same grid.
 Diagnostic for the multi-GPU path (the 8-GPU run belongs to the driver).
 """
 import argparse
-import json
 import os
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import jsonl  # noqa: E402
+
+
+def result(args, rank, obj):
+    """A rank's verdict goes to its own file; the launcher prints the merged
+    records from one process after every rank has exited (r4: two ranks'
+    prints into one inherited pipe interleaved)."""
+    jsonl.append_record(os.path.join(args.result_dir, f"rank{rank}.jsonl"), obj)
+
+
+def selftest(args, rank):
+    """CPU guard for the output path (tests/test_bench_helpers.py): each rank
+    emits --lines records straight to the shared stdout through jsonl.emit and
+    the same number through its result file."""
+    for i in range(args.lines):
+        rec = {"rank": rank, "i": i, "via": "stdout", "pad": "x" * (64 + 37 * (i % 7))}
+        jsonl.emit(rec)
+        result(args, rank, dict(rec, via="file"))
 
 
 def worker(args):
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if args.mode == "selftest":
+        selftest(args, rank)
+        return
     # before the RCCL library initialises: one "host" per rank, sockets on lo
     os.environ["NCCL_HOSTID"] = f"cfd-loopback-rank{rank}"
     # the ranks share one GPU; persistent solves stay on (the ticketed launch
@@ -106,7 +128,7 @@ def worker(args):
                            "sharded_wall_s": round(el, 3)})
     if rank == 0:
         for r in report:
-            print(json.dumps(r), flush=True)
+            result(args, rank, r)
         if not all(r["bitwise_equal_single_domain"] for r in report):
             sys.exit(1)
     dist.barrier()
@@ -181,7 +203,7 @@ def developed(args, rank, n, cfdamd, dist, np):
     # the p' rows either side of this slab's internal boundaries
     rows = ([j0 - 1, j0] if j0 > 0 else []) + ([j1 - 1, j1] if j1 < args.ny else [])
     nzf = float(np.count_nonzero(pp[rows])) / max(len(rows) * nx, 1) if rows else None
-    print(json.dumps({"case": "developed cavity, fixed-count (deep halos, overlapped exchange)",
+    result(args, rank, {"case": "developed cavity, fixed-count (deep halos, overlapped exchange)",
                       "rank": rank, "ranks": n, "ranks_seen": ranks_seen,
                       "grid": [args.nx, args.ny], "slab": [j0, j1], "develop": args.develop,
                       "steps": args.steps, "boundary_rows": rows,
@@ -189,7 +211,7 @@ def developed(args, rank, n, cfdamd, dist, np):
                       "developed_pprime_nonzero_frac": nz_dev,
                       "bitwise_equal_single_domain": not bad, "differ": bad,
                       "persist_blocks": persist_blocks,
-                      "sharded_wall_s": round(el, 3)}), flush=True)
+                      "sharded_wall_s": round(el, 3)})
     dist.barrier()
     dist.destroy_process_group()
     if bad:
@@ -203,9 +225,11 @@ def main():
     ap.add_argument("--ny", type=int, default=200)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--mode", default="both",
-                    choices=["fixed", "tol", "both", "solvers", "developed"])
+                    choices=["fixed", "tol", "both", "solvers", "developed", "selftest"])
     ap.add_argument("--develop", type=int, default=400)
     ap.add_argument("--timeout", type=float, default=240.0)
+    ap.add_argument("--lines", type=int, default=200)
+    ap.add_argument("--result-dir", default=None)
     ap.add_argument("--worker", action="store_true")
     args = ap.parse_args()
     if args.worker:
@@ -215,13 +239,15 @@ def main():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    rdir = tempfile.mkdtemp(prefix="cfd_rccl_loopback_")
     procs = []
     for r in range(args.n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.n), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), LOCAL_RANK="0")
         cmd = [sys.executable, os.path.abspath(__file__), "--worker", "--n", str(args.n),
                "--nx", str(args.nx), "--ny", str(args.ny), "--steps", str(args.steps),
-               "--mode", args.mode, "--develop", str(args.develop)]
+               "--mode", args.mode, "--develop", str(args.develop),
+               "--lines", str(args.lines), "--result-dir", rdir]
         procs.append(subprocess.Popen(cmd, env=env))
     rc = 0
     for p in procs:
@@ -230,6 +256,14 @@ def main():
         except subprocess.TimeoutExpired:
             p.kill()
             rc |= 1
+    # one process prints every rank's records, in rank order, one write each
+    for r in range(args.n):
+        path = os.path.join(rdir, f"rank{r}.jsonl")
+        for rec in jsonl.read_records(path):
+            jsonl.emit(rec)
+        if os.path.exists(path):
+            os.remove(path)
+    os.rmdir(rdir)
     sys.exit(rc)
 
 
