@@ -225,6 +225,19 @@ bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int
                          int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s);
 void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
                 int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0);
+// r5: an 8-sweep block of a single-domain solve as the chained march
+// (cfd_jacobi_chain.hip: a workgroup's four wave segments hand their boundary
+// rows to each other instead of recomputing cones); false: its plan does not
+// fit (nothing launched).  chain_enabled(): CFD_JACOBI_CHAIN (default on).
+bool launch_lds_chain8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
+                       uint32_t *rs, hipStream_t s);
+bool chain_enabled();
+// the chain runs the 8-sweep blocks over rows [out_lo, out_hi) of this grid
+bool chain_applies(const Geom &g, int out_lo, int out_hi);
+// its plan: wave columns, row groups per column, the chain groups' D (d0; the
+// first nhi groups d0 + 1) and the first (edge) group's rows
+bool chain_plan(const Geom &g, int out_lo, int out_hi, int occ, int *nwc, int *ngrp, int *d0, int *nhi,
+                int *elo);
 // Speculative temporal blocking for the tolerance mode (model.rs:748-819):
 // the launch starting at sweep `it` runs T sweeps (kind 5) and publishes
 // every sweep's residual; k_spec_check folds them, finds the first sweep

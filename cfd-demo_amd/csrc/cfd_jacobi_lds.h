@@ -489,7 +489,8 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           int nst, int bid, int spec_fold = 0,
                                           float *trk = nullptr, uint32_t *gset = nullptr,
                                           uint32_t *grhs = nullptr, const uint32_t *gprev = nullptr,
-                                          float plim = 0.0f, float rlim = 0.0f) {
+                                          float plim = 0.0f, float rlim = 0.0f, int r0o = -1,
+                                          int r1o = -1) {
     using M = LdsMarch<T, FAST, MODE, SUMS, GRD>;
     constexpr bool RES = M::RES;
     M w;
@@ -505,8 +506,9 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     // first / last one (lighter where that segment runs the boundary-row path)
     const long total = nseg == 1 ? 16 : wlo + whi + 16L * (nseg - 2);
     auto cum = [&](int i) -> long { return i <= 0 ? 0 : (i >= nseg ? total : wlo + 16L * (i - 1)); };
-    const int r0 = out_lo + (int)(cum(seg) * nrows / total);
-    const int r1 = out_lo + (int)(cum(seg + 1) * nrows / total);
+    // r0o >= 0: the caller's rows for this wave (k_jacobi_chain's edge groups)
+    const int r0 = r0o >= 0 ? r0o : out_lo + (int)(cum(seg) * nrows / total);
+    const int r1 = r0o >= 0 ? r1o : out_lo + (int)(cum(seg + 1) * nrows / total);
     if (r0 >= r1) return;
     const int nx = g.nx;
     w.ring = lds + wave * M::D * 64;

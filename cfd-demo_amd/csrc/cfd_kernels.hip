@@ -1621,10 +1621,20 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
         launch_pipe4(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else if (g.tb_kind == 4)
         launch_pipe2(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
-    else if (g.tb_kind == 5)
+    else if (g.tb_kind == 5) {
+        // r5: the chained march (cfd_jacobi_chain.hip) where its plan fits
+        if (T == 8 && chain_enabled() && launch_lds_chain8(g, f, pass, par, out_lo, out_hi, rs, s))
+            return;
         launch_lds(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
-    else
+    } else
         launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
+}
+
+// CFD_JACOBI_CHAIN=0: every 8-sweep block as the per-launch march (read per
+// call so tests can switch it)
+bool chain_enabled() {
+    const char *e = getenv("CFD_JACOBI_CHAIN");
+    return !(e && atoi(e) == 0);
 }
 
 bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,

@@ -1444,11 +1444,16 @@ struct cfd_model {
         const char *e = getenv("CFD_PERSIST_RES");
         return !(e && atoi(e) == 0);
     }();
-    // slabs: the blocks between two p' exchanges as one persistent launch
-    // (CFD_PERSIST_SHARDED=0: per launch)
+    // slabs: the blocks between two p' exchanges as one persistent launch,
+    // opt-in (CFD_PERSIST_SHARDED=1).  r5 same-geometry A/B (the rank slabs'
+    // owned rows + 2 x 32 ghost rows, the 24 KiB pad they get; medians of 3,
+    // profiles/r5/prof_r5b/slab_*.log): per launch 5.08 / 5.30 / 5.18 us per
+    // sweep against persistent 5.42 / 5.72 / 5.44 on the 4096^2, 8192 x 2112
+    // and 16384 x 1088 shapes, so every slab of the weak-scaling series runs
+    // one launch per 8-sweep block between its exchanges
     bool persist_sharded_env = [] {
         const char *e = getenv("CFD_PERSIST_SHARDED");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     // serialize persistent launches of different models on one device
     // (CFD_PERSIST_GATE=1; see launch_persist)
@@ -2745,6 +2750,7 @@ int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal) {
 
 int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len) {
     if (!m) return fail(CFD_EINVAL, "null model");
+    (void)hipSetDevice(m->device);   // chain_applies asks the occupancy API
     const bool spec = m->spec_mode();
     const bool resident = m->resident_mode();
     const int T = spec ? kMaxTemporal : m->g.tol_enabled ? 1 : m->t_max;
@@ -2760,6 +2766,9 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
             snprintf(buf, sizeof buf, "k_jacobi<%d, %d>", kJacRowsPerWave, m->g.fastdiv);
         else if (k == 1)
             snprintf(buf, sizeof buf, "k_jacobi_tb<%d, %d>", T, m->g.fastdiv);
+        else if (k == 5 && T == 8 && !m->sharded() &&
+                 chain_applies(m->g, 1 - (int)m->j0, (int)m->g.ny - 1 - (int)m->j0))
+            snprintf(buf, sizeof buf, "k_jacobi_chain<%d, %d, 0>", T, m->g.fastdiv);
         else if (k == 5)
             snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, 0>", T, m->g.fastdiv);
         else
@@ -2810,6 +2819,18 @@ int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks) {
     return 0;
 }
 
+int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks) {
+    if (!m) return fail(CFD_EINVAL, "null model");
+    int rc = m->sync();
+    if (rc) return rc;
+    uint32_t w[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpy(w, m->f.guard_slots + (size_t)kGuardSets * kResSlots * kResStride, 12,
+                      hipMemcpyDeviceToHost));
+    if (launches) *launches = w[1];
+    if (fallbacks) *fallbacks = w[2];
+    return 0;
+}
+
 int cfd_get_resident_solves(const cfd_model *m, uint64_t *solves) {
     if (!m || !solves) return fail(CFD_EINVAL, "null argument");
     *solves = m->resident_solves;
@@ -2848,6 +2869,15 @@ int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, i
 int cfd_plan_overlap(int nyl, int halo_depth, int rank, int n_ranks, int lo, int hi, int *out6) {
     if (!out6 || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad plan_overlap arguments");
     return plan_overlap(nyl, halo_depth, rank, n_ranks, lo, hi, out6);
+}
+
+int cfd_plan_chain(int nx, int ny, int n_cu, int occ, int out_lo, int out_hi, int *nwc, int *ngrp,
+                   int *d0, int *nhi, int *elo) {
+    if (nx < 2 || ny < 2 || n_cu < 1 || occ < 1 || !nwc || !ngrp || !d0 || !nhi || !elo)
+        return fail(CFD_EINVAL, "bad plan_chain arguments");
+    Geom g{};
+    g.nx = nx, g.ny = ny, g.j0 = 0, g.nyl = ny, g.n_cu = n_cu;
+    return chain_plan(g, out_lo, out_hi, occ, nwc, ngrp, d0, nhi, elo) ? 1 : 0;
 }
 
 int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6) {

@@ -372,12 +372,15 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     rhs_huge[500:520, 300:340] = np.float32(2.0 ** 126)
     cases = {"plain": {}, "huge_pp": {"p_prime": pp_huge.ravel()},
              "huge_rhs": {"rhs": rhs_huge.ravel()}}
-    envs = {"per_launch": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "0"},
-            "per_launch_sums": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "1"},
-            "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0"},
-            "sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "1"}}
+    envs = {"per_launch": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "0", "CFD_JACOBI_CHAIN": "0"},
+            "per_launch_sums": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "1", "CFD_JACOBI_CHAIN": "0"},
+            "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0", "CFD_JACOBI_CHAIN": "0"},
+            "sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "1", "CFD_JACOBI_CHAIN": "0"},
+            # r5: the chained march (default), optimistic SUMS per row group
+            "chain": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "1", "CFD_JACOBI_CHAIN": "1"}}
     per_launch_sums = {}
     sums = {}
+    chain_fb = {}
     for name, inject in cases.items():
         out = {}
         for key, env in envs.items():
@@ -388,6 +391,10 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
                 mm.set_state(**dict(base, **inject))
                 mm.jacobi_pressure()
                 out[key] = (mm.get_state()["p_prime"], mm.persist_blocks, mm.persist_sums)
+                if key == "chain":
+                    cs = mm.chain_stats
+                    assert cs["launches"] == 25, cs
+                    chain_fb[name] = cs["fallbacks"]
             finally:
                 mm.close()
         for key, (pp, _, _) in out.items():
@@ -402,3 +409,6 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     # plain: the owned tiles' blocks 2..24 (blocks 0 and 1 measure the inputs)
     assert sums["plain"] > 0, sums
     assert 0 < sums["huge_pp"] < sums["plain"] and 0 < sums["huge_rhs"] < sums["plain"], sums
+    # the chain re-runs exactly the row groups that read a huge value, in the
+    # reference's form (every launch of the huge cases has some; none plain)
+    assert chain_fb["plain"] == 0 and chain_fb["huge_pp"] > 0 and chain_fb["huge_rhs"] > 0, chain_fb

@@ -121,6 +121,6 @@ def test_rccl_developed_full_size_slabs_bitwise(n, nx, ny):
         assert x["bitwise_equal_single_domain"], x
         assert x["ranks_seen"] == n
         assert x["boundary_pprime_nonzero_frac"] >= 0.9, x
-        # persistent runs between the p' exchanges, beside the other ranks'
-        # kernels on the shared GPU: the SCALE configuration (r4)
-        assert x["persist_blocks"] >= 2, x
+        # the SCALE configuration since r5: one launch per 8-sweep block
+        # between the p' exchanges (the same-geometry A/B)
+        assert x["persist_blocks"] == 0, x

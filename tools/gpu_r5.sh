@@ -57,9 +57,11 @@ if has ab; then
 fi
 if has abslab; then
   # persistent vs per-launch on the exact rank geometries (tb_one slab proxies
-  # carry the owned rows + 2 x hg ghost rows and get the owned-row pad)
+  # carry the owned rows + 2 x hg ghost rows; the pad is forced to the 24 KiB
+  # the real slab gets from its OWNED rows -- the 16384 x 1088 proxy would
+  # otherwise fall past the cache threshold and run unpadded)
   for shape in ${SLAB_SHAPES:-4096 8192x2112@4096 16384x1088@8192}; do
-    step slab_$shape 420 env AB_CMD="tb_one.py $shape 5" TB_WARMUP=300 AB_ROUNDS=3 python3 -u tools/ab_env.py "CFD_PERSIST=0" "CFD_PERSIST=1"
+    step slab_$shape 420 env AB_CMD="tb_one.py $shape 5" TB_WARMUP=300 AB_ROUNDS=3 python3 -u tools/ab_env.py "CFD_PERSIST=0,CFD_LDS_PAD=24576" "CFD_PERSIST=1,CFD_LDS_PAD=24576"
   done
 fi
 echo "=== done"

@@ -51,8 +51,7 @@ def worker(args):
         return
     # before the RCCL library initialises: one "host" per rank, sockets on lo
     os.environ["NCCL_HOSTID"] = f"cfd-loopback-rank{rank}"
-    # the ranks share one GPU; persistent solves stay on (the ticketed launch
-    # completes beside the other rank's kernels): the SCALE configuration
+    # the ranks share one GPU
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.setdefault("NCCL_NET", "Socket")
@@ -194,7 +193,7 @@ def developed(args, rank, n, cfdamd, dist, np):
     el = time.perf_counter() - t0
     got = m.get_state()
     ranks_seen = m.comm_size
-    persist_blocks = m.persist_blocks   # the persistent runs between exchanges (SCALE config)
+    persist_blocks = m.persist_blocks   # persistent blocks (0: per launch, the SCALE config)
     m.close()
     exp = slab_slices(want, nx, j0, j1)
     bad = [k for k in ("u", "v", "p", "p_prime", "u_star", "v_star", "rhs")
