@@ -228,7 +228,7 @@ void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par
 // r5: an 8-sweep block of a single-domain solve as the chained march
 // (cfd_jacobi_chain.hip: a workgroup's four wave segments hand their boundary
 // rows to each other instead of recomputing cones); false: its plan does not
-// fit (nothing launched).  chain_enabled(): CFD_JACOBI_CHAIN (default on).
+// fit (nothing launched).  chain_enabled(): CFD_JACOBI_CHAIN=1 (opt-in).
 bool launch_lds_chain8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
                        uint32_t *rs, hipStream_t s);
 bool chain_enabled();

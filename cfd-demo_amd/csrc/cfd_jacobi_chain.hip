@@ -26,10 +26,15 @@
 //     partner's stage s-1 value of the partner's first row, sent at slot s);
 //   end meeting: stage s ends at slot D+s with row D, whose upper neighbour
 //     is the partner's stage s-1 value of ITS last row (sent at slot D+s-1).
-// Every wave of the group has the same slot count D+T+1, so the hand-offs and
-// their workgroup barriers (slots 2..T and D+1..D+T-1) line up.  Each value
-// is the reference's: a stage reads exactly the neighbours the reference's
-// sweep reads, computed by exactly the reference's expression.
+// Every wave of the group has the same slot count D+T+1.  A hand-off is one
+// LDS row per (wave, meeting, stage) and a per-(wave, meeting) flag holding
+// the last stage published: the producer never waits (every row has its own
+// entry), the consumer polls the flag only when it needs the row, one slot
+// after the partner produced it (workgroup barriers at every hand-off slot
+// measured 5.88 vs 4.99 us per sweep: each forced the group's four SIMDs
+// into lockstep).  Each value is the reference's: a stage reads exactly the
+// neighbours the reference's sweep reads, computed by exactly the
+// reference's expression.
 //
 // The first and last row group of every wave column (whose rows reach the
 // global boundary rows, or are too few for a chain) run the per-launch march
@@ -48,8 +53,24 @@
 namespace cfd {
 namespace {
 
+constexpr int kChainStages = 8;   // hand-off rows per (wave, meeting): stages 1..T-1, T <= 8
+
+// CFD_CHAIN_STAMP (diagnostic builds only, tools/chain_stamps.py): every wave
+// records s_memrealtime at its start, the end of its opening, the end of its
+// steady slots, the end of its march and its exit, plus its HW_ID / XCC_ID,
+// role and row group (vector stores into g_chain_stamp)
+#ifndef CFD_CHAIN_STAMP
+#define CFD_CHAIN_STAMP 0
+#endif
+#if CFD_CHAIN_STAMP
+constexpr int kChainStampWaves = 1 << 15;
+__device__ unsigned long long g_chain_stamp[kChainStampWaves * 8];
+__device__ __forceinline__ unsigned long long chain_now() { return __builtin_amdgcn_s_memrealtime(); }
+#endif
+
 template <int T, int FAST, bool RES, bool SUMS, bool WARM, int E>
 struct ChainMarch {
+    static_assert(T <= kChainStages, "hand-off rows");
     static constexpr int NW = 3;
     static constexpr int PD = CFD_LDS_PD;
     static constexpr int DR = ring_depth(T, PD, 1);   // rhs ring rows (9 at T = 8)
@@ -58,21 +79,24 @@ struct ChainMarch {
     static constexpr int OUTL = 64 - 2 * H;
     static constexpr int kCol = 1;
     static constexpr int PLD_AUX = CFD_LDS_LD_AUX, PST_AUX = CFD_LDS_ST_AUX;
-    // first slot of stage s; slots from P0 on run every stage
+    // first slot of stage s; the opening runs slots [0, P0): through stage
+    // T's first slot (after a meeting start, that slot still takes a hand-off)
     static constexpr int st0(int s) { return WARM ? 2 * s : s + 1; }
-    static constexpr int P0 = WARM ? 2 * T : T + 1;
+    static constexpr int P0 = st0(T) + (WARM ? 0 : 1);
     static_assert(DR % NW == 0 && DR % PD == 0 && DR >= T + 1, "ring geometry");
 
     f2 W[T][NW];   // W[s][v % NW]: stage s's row of slot v
     f2 PQ[PD], RQ[PD];
     f2 *ring;      // this wave's rhs ring (LDS)
-    f2 *xb;        // the group's hand-off rows: [wave][meeting][parity][64 lanes]
+    f2 *xb;        // the group's hand-off rows: [wave][meeting][stage][64 lanes]
+    uint32_t *xf;  // [wave][meeting]: the last stage published
     int lane, wave, ps, pe;   // partner wave of the start / end meeting
     int Dd, S, abase, dir, ch, nch, vo_ld, vo_st, row_bytes, wbase, lo_clamp, hi_clamp, nyl_;
     bool e0, e1;
     float dx_sq, r_dx_sq, dy_sq, r_dy_sq, denom, r_denom;
     __amdgpu_buffer_rsrc_t rs_p, rs_r, rs_d;
     float m, imax, rmax;
+    unsigned long long t_open = 0, t_steady = 0, t_march = 0;   // CFD_CHAIN_STAMP
 
     __device__ __forceinline__ int act(int vrow) const { return abase + dir * vrow; }
 
@@ -114,30 +138,32 @@ struct ChainMarch {
         return o;
     }
 
-    // one row per (wave, meeting, slot parity): a wave's start partner may
-    // still read its start hand-off while its end partner's begins (no barrier
-    // between the two phases)
-    __device__ __forceinline__ void send(const f2 &n, int ph, int par) const {
-        xb[((wave * 2 + ph) * 2 + par) * 64 + lane] = n;
+    // stage s's row for the partner: the row, then the flag (workgroup-scope
+    // release: the row's LDS write has completed; no wait on global loads)
+    __device__ __forceinline__ void send(const f2 &n, int ph, int s) const {
+        xb[((wave * 2 + ph) * kChainStages + s) * 64 + lane] = n;
+        __hip_atomic_store(&xf[wave * 2 + ph], (uint32_t)s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __device__ __forceinline__ f2 recv(int partner, int ph, int par) const {
-        return xb[((partner * 2 + ph) * 2 + par) * 64 + lane];
-    }
-    // the hand-off: LDS writes drained, every wave of the group arrived (no
-    // wait on the global loads in flight: the workgroup fences compile to
-    // s_waitcnt lgkmcnt(0) + s_barrier on gfx950)
-    static __device__ __forceinline__ void barrier() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // the partner's stage s row, once its flag says it is there (the partner
+    // is in this workgroup and produces it without waiting on us; the poll is
+    // bounded all the same)
+    __device__ __forceinline__ f2 recv(int partner, int ph, int s) const {
+#pragma unroll 1
+        for (int k = 0; k < (1 << 22); ++k) {
+            const uint32_t fl = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&xf[partner * 2 + ph], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if ((int)fl >= s) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return xb[((partner * 2 + ph) * kChainStages + s) * 64 + lane];
     }
 
     // Slot v (V_ == v mod U).  PH 0: the opening slots (V_ == v, compile-time
     // stage ramp and start hand-offs); 1: steady (every stage, no hand-off);
-    // 2: the closing slots (run-time: stage s ends at slot Dd + s).
+    // 3: steady, skipped past slot Dd (the remainder before the closing).
     template <int V_, int PH>
     __device__ __forceinline__ void slot(int v) {
-        if (PH == 2 && v >= S) return;
+        if (PH == 3 && v > Dd) return;
         const int k = v;
         W[0][V_ % NW] = PQ[V_ % PD];
         PQ[V_ % PD] = ld<PLD_AUX>(rs_p, k + PD);
@@ -147,52 +173,107 @@ struct ChainMarch {
 #pragma unroll
         for (int s = 1; s <= T; ++s) {
             if (PH == 0 && V_ < st0(s)) continue;   // compile-time
-            if (PH == 2 && v > Dd + s) continue;    // wave-uniform: stage s is done
             if constexpr (PH == 0 && !WARM) {
                 // the first row's lower neighbour: the partner's stage s-1
                 // value of its own first row
-                if (s >= 2 && V_ == st0(s)) W[s - 1][(V_ - 2 + kW) % NW] = recv(ps, 0, (V_ - 1) & 1);
+                if (s >= 2 && V_ == st0(s)) W[s - 1][(V_ - 2 + kW) % NW] = recv(ps, 0, s - 1);
             }
-            if (PH == 2 && s >= 2 && v == Dd + s)   // the last row's upper neighbour
-                W[s - 1][V_ % NW] = recv(pe, 1, (v - 1) & 1);
             const f2 rh = ring[((V_ - s + 8 * DR) % DR) * 64 + lane];
-            const f2 &B = W[s - 1][(V_ - 2 + kW) % NW];
-            const f2 &C = W[s - 1][(V_ - 1 + kW) % NW];
-            const f2 &Tp = W[s - 1][V_ % NW];
-            if constexpr (SUMS) {
-                if (s == 1) {   // every input row once (plus the first two), every rhs row
-                    imax = fmaxf(fmaxf(imax, fabsf(Tp.x)), fabsf(Tp.y));
-                    rmax = fmaxf(fmaxf(rmax, fabsf(rh.x)), fabsf(rh.y));
-                    if (PH == 0 && V_ == st0(1))
-                        imax = fmaxf(fmaxf(imax, fmaxf(fabsf(B.x), fabsf(B.y))),
-                                     fmaxf(fabsf(C.x), fabsf(C.y)));
-                }
-            }
-            const f2 n = update(B, C, Tp, rh);
-            if (s < T) {
+            const f2 n = stage_at(s, W[s - 1][(V_ - 2 + kW) % NW], W[s - 1][(V_ - 1 + kW) % NW],
+                                  W[s - 1][V_ % NW], rh, PH == 0 && V_ == st0(1));
+            if (s < T)
                 W[s][V_ % NW] = n;
-            } else {
-                const int ra = act(v - T);
-                if (RES) {
-                    const f2 d = n - C;
-                    if (!(E & kCol)) {
-                        m = fmaxf(fmaxf(m, fabsf(d.x)), fabsf(d.y));
-                    } else {
-                        if (e0) m = fmaxf(m, fabsf(d.x));
-                        if (e1) m = fmaxf(m, fabsf(d.y));
-                    }
-                }
-                st(n, ra);
-            }
+            else
+                store_row(n, W[s - 1][(V_ - 1 + kW) % NW], act(v - T));
             if constexpr (PH == 0 && !WARM) {
-                if (s <= T - 1 && V_ == st0(s)) send(n, 0, V_ & 1);
+                if (s <= T - 1 && V_ == st0(s)) send(n, 0, s);
             }
-            if (PH == 2 && s <= T - 1 && v == Dd + s) send(n, 1, v & 1);
         }
-        if constexpr (PH == 0) {
-            if (V_ >= 2 && V_ <= T) barrier();
+    }
+
+    // stage s's update with the SUMS form's input tracking (stage 1 sees
+    // every input row once as Tp, its first slot the first two as B and C)
+    __device__ __forceinline__ f2 stage_at(int s, const f2 &B, const f2 &C, const f2 &Tp, const f2 &rh,
+                                           bool first) {
+        if constexpr (SUMS) {
+            if (s == 1) {
+                imax = fmaxf(fmaxf(imax, fabsf(Tp.x)), fabsf(Tp.y));
+                rmax = fmaxf(fmaxf(rmax, fabsf(rh.x)), fabsf(rh.y));
+                if (first)
+                    imax = fmaxf(fmaxf(imax, fmaxf(fabsf(B.x), fabsf(B.y))),
+                                 fmaxf(fabsf(C.x), fabsf(C.y)));
+            }
         }
-        if (PH == 2 && v >= Dd + 1 && v <= Dd + T - 1) barrier();
+        return update(B, C, Tp, rh);
+    }
+    // stage T's row: the residual (RES) and the store
+    __device__ __forceinline__ void store_row(const f2 &n, const f2 &C, int ra) {
+        if (RES) {
+            const f2 d = n - C;
+            if (!(E & kCol)) {
+                m = fmaxf(fmaxf(m, fabsf(d.x)), fabsf(d.y));
+            } else {
+                if (e0) m = fmaxf(m, fabsf(d.x));
+                if (e1) m = fmaxf(m, fabsf(d.y));
+            }
+        }
+        st(n, ra);
+    }
+
+    // The closing: slots Dd+1 .. Dd+T, compile-time.  Slot Dd+J runs stages
+    // J..T; stage J makes row Dd (the last) from the partner's stage J-1 row
+    // and hands its own on.  No loads: the last input row (Dd+1) was
+    // prefetched, and every rhs row a closing stage reads is in the ring.
+    // The register rings are first rotated so that slot Dd+1 sits at index 0
+    // (a 3-way switch, once per wave); the LDS ring is addressed at run time.
+    template <int R>
+    __device__ __forceinline__ void rotate() {
+        // new[i] = old[(i + R) % 3]
+        if constexpr (R != 0) {
+#pragma unroll
+            for (int q = 0; q < T; ++q) {
+                const f2 a0 = W[q][R % NW], a1 = W[q][(1 + R) % NW], a2 = W[q][(2 + R) % NW];
+                W[q][0] = a0, W[q][1] = a1, W[q][2] = a2;
+            }
+            const f2 p0 = PQ[R % PD], p1 = PQ[(1 + R) % PD], p2 = PQ[(2 + R) % PD];
+            PQ[0] = p0, PQ[1] = p1, PQ[2] = p2;
+        }
+    }
+    template <int J>
+    __device__ __forceinline__ void closing_slot(int r9) {
+        // W index of slot Dd+J after the rotation: (J-1) % NW
+        constexpr int I0 = (J - 1) % NW, Im1 = (J - 2 + NW) % NW, Im2 = (J - 3 + 2 * NW) % NW;
+        if (J == 1) W[0][I0] = PQ[0];   // input row Dd+1
+#pragma unroll
+        for (int s = J; s <= T; ++s) {
+            if (s >= 2 && s == J) W[s - 1][I0] = recv(pe, 1, s - 1);   // the last row's upper neighbour
+            // rhs row Dd+J-s sits in ring slot (Dd+J-s) mod DR, r9 = (Dd+1) mod DR
+            int q = r9 + J - 1 - s;   // in [r9 - T, r9 - 1]
+            q = q < 0 ? q + DR : q;
+            const f2 rh = ring[q * 64 + lane];
+            const f2 n = stage_at(s, W[s - 1][Im2], W[s - 1][Im1], W[s - 1][I0], rh, false);
+            if (s < T)
+                W[s][I0] = n;
+            else
+                store_row(n, W[s - 1][Im1], act(Dd + J - T));
+            if (s == J && s <= T - 1) send(n, 1, s);
+        }
+    }
+    template <int J>
+    __device__ __forceinline__ void closing(int r9) {
+        if constexpr (J <= T) {
+            closing_slot<J>(r9);
+            closing<J + 1>(r9);
+        }
+    }
+    __device__ __forceinline__ void close_march() {
+        // slot Dd+1's register-ring index before the rotation
+        const int phi = (Dd + 1) % NW;
+        if (phi == 1)
+            rotate<1>();
+        else if (phi == 2)
+            rotate<2>();
+        closing<1>((Dd + 1) % DR);
     }
 
     template <int V_>
@@ -225,22 +306,31 @@ struct ChainMarch {
     __device__ __forceinline__ void run() {
         set_prio(0);
         opening<0>();
+#if CFD_CHAIN_STAMP
+        t_open = chain_now();
+#endif
         int base = P0;
         for (; base + U <= Dd + 1; base += U) {   // every slot of the group <= Dd
             set_prio(base - P0);
             group<0, 1>(base);
         }
+#if CFD_CHAIN_STAMP
+        t_steady = chain_now();
+#endif
         set_prio(base - P0);
-        group<0, 2>(base);   // at most U - 1 steady slots + T closing slots
-        group<0, 2>(base + U);
+        group<0, 3>(base);   // the steady slots left before the closing (< U)
+        close_march();
+#if CFD_CHAIN_STAMP
+        t_march = chain_now();
+#endif
     }
 };
 
 // A chain wave's march in form SUMS; returns its (wave-max) guard maxima.
 template <int T, int FAST, bool RES, bool SUMS, bool WARM, int E>
 __device__ __forceinline__ void chain_run(const Geom &g, float *src_alloc, float *dst_alloc,
-                                          const float *rhs, f2 *lds, int wave, int lane, int wc,
-                                          int Dd, int abase, int dir, int ps, int pe, float *im,
+                                          const float *rhs, f2 *lds, uint32_t *xflags, int wave, int lane,
+                                          int wc, int Dd, int abase, int dir, int ps, int pe, float *im,
                                           float *rm, float *mres) {
     using M = ChainMarch<T, FAST, RES, SUMS, WARM, E>;
     M w;
@@ -254,6 +344,7 @@ __device__ __forceinline__ void chain_run(const Geom &g, float *src_alloc, float
     w.dir = dir;
     w.ring = lds + wave * M::DR * 64;
     w.xb = lds + kLdsWaves * M::DR * 64;
+    w.xf = xflags;
     const int nx = g.nx;
     w.nch = nx / 2;
     w.nyl_ = g.nyl;
@@ -297,6 +388,14 @@ __device__ __forceinline__ void chain_run(const Geom &g, float *src_alloc, float
         w.RQ[q] = w.ld(w.rs_r, q);
     }
     w.run();
+#if CFD_CHAIN_STAMP
+    if (!RES && lane == 0 && (int)blockIdx.x * kLdsWaves + wave < kChainStampWaves) {
+        unsigned long long *p = g_chain_stamp + ((size_t)blockIdx.x * kLdsWaves + wave) * 8;
+        p[1] = w.t_open;
+        p[2] = w.t_steady;
+        p[3] = w.t_march;
+    }
+#endif
     *im = wave_max(in_dom ? w.imax : 0.0f);
     *rm = wave_max(in_dom ? w.rmax : 0.0f);
     *mres = wave_max(out_lane ? w.m : 0.0f);
@@ -304,25 +403,25 @@ __device__ __forceinline__ void chain_run(const Geom &g, float *src_alloc, float
 
 template <int T, int FAST, bool RES, bool SUMS, int E>
 __device__ __forceinline__ void chain_role(const Geom &g, float *src, float *dst, const float *rhs, f2 *lds,
-                                           int wave, int lane, int wc, int Dd, int abase, int dir, int ps,
+                                           uint32_t *xflags, int wave, int lane, int wc, int Dd, int abase, int dir, int ps,
                                            int pe, float *im, float *rm, float *mres) {
     if (wave == 0 || wave == kLdsWaves - 1)
-        chain_run<T, FAST, RES, SUMS, true, E>(g, src, dst, rhs, lds, wave, lane, wc, Dd, abase, dir, ps,
+        chain_run<T, FAST, RES, SUMS, true, E>(g, src, dst, rhs, lds, xflags, wave, lane, wc, Dd, abase, dir, ps,
                                                pe, im, rm, mres);
     else
-        chain_run<T, FAST, RES, SUMS, false, E>(g, src, dst, rhs, lds, wave, lane, wc, Dd, abase, dir, ps,
+        chain_run<T, FAST, RES, SUMS, false, E>(g, src, dst, rhs, lds, xflags, wave, lane, wc, Dd, abase, dir, ps,
                                                 pe, im, rm, mres);
 }
 
 template <int T, int FAST, bool RES, bool SUMS>
 __device__ __forceinline__ void chain_form(const Geom &g, float *src, float *dst, const float *rhs, f2 *lds,
-                                           int wave, int lane, int wc, bool col_edge, int Dd, int abase,
+                                           uint32_t *xflags, int wave, int lane, int wc, bool col_edge, int Dd, int abase,
                                            int dir, int ps, int pe, float *im, float *rm, float *mres) {
     if (col_edge)
-        chain_role<T, FAST, RES, SUMS, 1>(g, src, dst, rhs, lds, wave, lane, wc, Dd, abase, dir, ps, pe,
+        chain_role<T, FAST, RES, SUMS, 1>(g, src, dst, rhs, lds, xflags, wave, lane, wc, Dd, abase, dir, ps, pe,
                                           im, rm, mres);
     else
-        chain_role<T, FAST, RES, SUMS, 0>(g, src, dst, rhs, lds, wave, lane, wc, Dd, abase, dir, ps, pe,
+        chain_role<T, FAST, RES, SUMS, 0>(g, src, dst, rhs, lds, xflags, wave, lane, wc, Dd, abase, dir, ps, pe,
                                           im, rm, mres);
 }
 
@@ -337,10 +436,31 @@ __global__ __launch_bounds__(kLdsWaves * 64, 1) void k_jacobi_chain(
     int elo, int wlo, int whi, int sums, float plim, float rlim, uint32_t *cstat) {
     using MC = ChainMarch<T, FAST, MODE == 1, false, false, 0>;
     constexpr bool RES = MODE == 1;
-    __shared__ f2 lds[kLdsWaves * (MC::DR + 4) * 64];
+    // per wave: its rhs ring (DR rows), then every wave's hand-off rows
+    // (2 meetings x kChainStages), then the hand-off flags
+    __shared__ f2 lds[kLdsWaves * (MC::DR + 2 * kChainStages) * 64];
+    __shared__ uint32_t xflags[2 * kLdsWaves];
     __shared__ float gm[2 * kLdsWaves];
     __shared__ int redo_s;
     if (pass_off(ctl, pass)) return;
+#if CFD_CHAIN_STAMP
+    struct StampOnExit {
+        unsigned long long t0;
+        int role;
+        __device__ ~StampOnExit() {
+            const int idx = (int)blockIdx.x * kLdsWaves + ((int)threadIdx.x >> 6);
+            if (MODE == 0 && (threadIdx.x & 63) == 0 && idx < kChainStampWaves) {
+                unsigned long long *p = g_chain_stamp + (size_t)idx * 8;
+                const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+                const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+                p[0] = t0;
+                p[4] = chain_now();
+                p[5] = ((unsigned long long)xcc << 32) | hw;
+                p[6] = (unsigned long long)role;
+            }
+        }
+    } stamp_guard{chain_now(), 0};
+#endif
     const int bid = xcd_block(g);
     // diagnostics (cfd_get_chain_stats): chain launches, groups re-run in the
     // reference's form
@@ -348,6 +468,10 @@ __global__ __launch_bounds__(kLdsWaves * 64, 1) void k_jacobi_chain(
     const int wc = bid % nwc, grp = bid / nwc;
     if (grp >= ngrp) return;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+#if CFD_CHAIN_STAMP
+    // role: 0..3 chain waves, 4 edge group; the row group above it
+    stamp_guard.role = ((grp == 0 || grp == ngrp - 1) ? 4 : wave) | (grp << 8);
+#endif
     const int lane = (int)threadIdx.x & 63;
     const int M = ngrp - 2;
     const int r4_0 = 4 * d0 + 2 - 2 * T;   // rows of a chain group with D = d0
@@ -389,8 +513,11 @@ __global__ __launch_bounds__(kLdsWaves * 64, 1) void k_jacobi_chain(
     const bool col_edge = ch_lo <= 0 || 2 * (ch_hi + 1) > g.nx - 8;
     float im = 0.0f, rm = 0.0f, mres = 0.0f;
     bool done = false;
+    // the hand-off flags start at 0 (LDS is not cleared between workgroups)
+    if (threadIdx.x < 2 * kLdsWaves) xflags[threadIdx.x] = 0u;
+    __syncthreads();
     if (FAST == 1 && sums) {
-        chain_form<T, FAST, RES, (FAST == 1)>(g, src, dst, rhs, lds, wave, lane, wc, col_edge, Dd, abase,
+        chain_form<T, FAST, RES, (FAST == 1)>(g, src, dst, rhs, lds, xflags, wave, lane, wc, col_edge, Dd, abase,
                                              dir, ps, pe, &im, &rm, &mres);
         if (lane == 0) {
             gm[wave] = im;
@@ -410,10 +537,14 @@ __global__ __launch_bounds__(kLdsWaves * 64, 1) void k_jacobi_chain(
         if (threadIdx.x == 0) redo_s = done ? 0 : 1;
         __syncthreads();
         done = redo_s == 0;
-        if (!done && threadIdx.x == 0 && cstat) atomicAdd(cstat + 2, 1u);
+        if (!done) {
+            if (threadIdx.x == 0 && cstat) atomicAdd(cstat + 2, 1u);
+            if (threadIdx.x < 2 * kLdsWaves) xflags[threadIdx.x] = 0u;   // the re-run's hand-offs
+            __syncthreads();
+        }
     }
     if (!done)
-        chain_form<T, FAST, RES, false>(g, src, dst, rhs, lds, wave, lane, wc, col_edge, Dd, abase, dir,
+        chain_form<T, FAST, RES, false>(g, src, dst, rhs, lds, xflags, wave, lane, wc, col_edge, Dd, abase, dir,
                                         ps, pe, &im, &rm, &mres);
     if (RES && lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, mres);
 }
@@ -481,7 +612,10 @@ namespace {
 // workgroups per CU the chain launch's round is sized for
 int chain_occ(const Geom &g, int mode) {
     constexpr int T = 8;
-    const int pad = lds_pad_bytes(g, mode);
+    // no occupancy pad: the kernel's own LDS (rhs rings + hand-off rows,
+    // ~51 KB) and its ~130 VGPRs already hold it to 3 workgroups per CU
+    const int pad = 0;
+    (void)mode;
     int occ = 0;
 #define CFD_CHAIN_OCC(FV, MV) occ = chain_blocks_per_cu<T, FV, MV>(pad)
     if (g.fastdiv == 1) {
@@ -514,7 +648,10 @@ bool launch_lds_chain8(const Geom &g, const Fields &f, int pass, int par, int ou
     constexpr int T = 8;
     if (!chain_geom_ok(g)) return false;
     const int mode = rs ? 1 : 0;
-    const int pad = lds_pad_bytes(g, mode);
+    // no occupancy pad: the kernel's own LDS (rhs rings + hand-off rows,
+    // ~51 KB) and its ~130 VGPRs already hold it to 3 workgroups per CU
+    const int pad = 0;
+    (void)mode;
     const int occ = chain_occ(g, mode);
     int nwc, ngrp, d0, nhi, elo;
     if (!chain_plan(g, out_lo, out_hi, occ, &nwc, &ngrp, &d0, &nhi, &elo)) return false;
@@ -547,5 +684,13 @@ bool launch_lds_chain8(const Geom &g, const Fields &f, int pass, int par, int ou
 #undef CFD_CHAIN_LAUNCH
     return true;
 }
+
+#if CFD_CHAIN_STAMP
+extern "C" int cfd_diag_chain_stamps(unsigned long long *host, int nwaves) {
+    if (nwaves > kChainStampWaves) nwaves = kChainStampWaves;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chain_stamp), (size_t)nwaves * 64, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? nwaves : -1;
+}
+#endif
 
 }  // namespace cfd

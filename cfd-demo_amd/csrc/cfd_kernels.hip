@@ -1630,11 +1630,14 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
         launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
 }
 
-// CFD_JACOBI_CHAIN=0: every 8-sweep block as the per-launch march (read per
-// call so tests can switch it)
+// CFD_JACOBI_CHAIN=1: 8-sweep blocks of single-domain solves as the chained
+// march (opt-in: r5 measured it slower than the per-launch march, 5.48 vs
+// 4.95 us per sweep at 4096^2, profiles/r5/ -- its opening and closing slots
+// are as long as full ones, see cfd_jacobi_chain.hip).  Read per call so
+// tests can switch it.
 bool chain_enabled() {
     const char *e = getenv("CFD_JACOBI_CHAIN");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) != 0;
 }
 
 bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,

@@ -257,8 +257,8 @@ int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
 int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
 /* The chained 8-sweep march (k_jacobi_chain, r5: a workgroup's four wave
  * segments hand their boundary rows to each other instead of recomputing
- * warm-up cones; default for single-domain fixed-count solves where its
- * plan fits): launches run, and row groups whose optimistic SUMS form failed
+ * warm-up cones; opt-in CFD_JACOBI_CHAIN=1 for single-domain fixed-count
+ * solves where its plan fits): launches run, and row groups whose optimistic SUMS form failed
  * its guard and were re-run in the reference's form, summed over the model's
  * life.  Synchronises.  (new; diagnostics) */
 int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks);

@@ -1,5 +1,5 @@
-"""GPU: the chained 8-sweep march (k_jacobi_chain, cfd_jacobi_chain.hip, r5)
-against the oracle and against the per-launch march it replaces.  A
+"""GPU: the chained 8-sweep march (k_jacobi_chain, cfd_jacobi_chain.hip, r5;
+opt-in CFD_JACOBI_CHAIN=1) against the oracle and against the per-launch march it replaces.  A
 workgroup's four wave segments alternate direction and hand each other the
 boundary row each stage needs (start and end meetings through LDS); the
 first/last row group of every wave column runs the per-launch march.  Every
@@ -47,8 +47,13 @@ def _model(nx, ny, lx, ly, cyl, kw):
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_chain_matches_oracle(case):
+def test_chain_matches_oracle(monkeypatch, case):
     nx, ny, lx, ly, cyl, kw = CASES[case]
+    # kind 5 at 8 sweeps per launch on every grid (IEEE-division grids select
+    # kind 4 at T = 4 by default): the chain in all three division forms
+    monkeypatch.setenv("CFD_TB_KIND", "5")
+    monkeypatch.setenv("CFD_TEMPORAL", "8")
+    monkeypatch.setenv("CFD_JACOBI_CHAIN", "1")
     m = _model(nx, ny, lx, ly, cyl, kw)
     try:
         assert m.jacobi_kernel["name"].startswith("k_jacobi_chain"), m.jacobi_kernel
