@@ -467,6 +467,14 @@ class Model:
         return dict(launches=int(a.value), fallbacks=int(b.value))
 
     @property
+    def recoveries(self) -> int:
+        """Solve timeouts the model recovered from by itself: checkpoint
+        restored, calls since re-run per launch (cfd_get_recoveries)."""
+        n = C.c_uint64()
+        check("cfd_get_recoveries", load().cfd_get_recoveries(self._hh(), C.byref(n)))
+        return int(n.value)
+
+    @property
     def resident_solves(self) -> int:
         """Tolerance-mode solves enqueued as one resident launch
         (k_jacobi_resident; cfd_get_resident_solves)."""

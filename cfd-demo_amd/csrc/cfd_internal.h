@@ -70,7 +70,9 @@ struct Ctl {
     uint32_t n_exec_last;   // sweeps executed by the last solve
     float last_p;           // last_pressure_residual
     float res_u, res_v;     // last_u_residual / last_v_residual
-    uint32_t red[6];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|; red[5]: the last
+    uint32_t red[7];        // step maxima as f32 bits: |du|, |dv|, |u|, |v|; red[6]: a
+                            // persistent solve of some slab timed out (r5, all-reduced so
+                            // every rank recovers); red[5]: the last
                             // solve's residual (all-reduced with the maxima on slabs); red[4]:
                             // non-finite flag (1: some new u/v value is NaN or +-Inf)
     uint32_t nonfinite_step;   // sticky: simulation_step after the first step whose
@@ -125,8 +127,6 @@ struct Geom {
                           // 0: separate launches; where the fused forms apply
     int32_t res_div;      // r4: the resident solve's division mode: fastdiv, or 3 (FMA-corrected
                           // above 2^-96, IEEE below; proven like the others) where fastdiv is 0
-    int32_t guard_par0;   // r4: the solve's first k_jacobi_lds launch index of a guarded
-                          // chain (the SUMS form's guard, Fields::guard_slots); -1: none
 };
 
 struct Fields {
@@ -150,10 +150,10 @@ struct Fields {
     // the RCCL watchdog's evidence of forward progress
     uint32_t *host_progress;
     uint32_t *persist;   // kPersistWords words after the slot sets (see kPersistFlagStride)
-    // r4: the per-launch solve's SUMS guard, kGuardSets spread sets: sets 0..3
-    // a ring of max |p'| the chain's launch g stores (set g & 3), set 4 max
-    // |rhs| (its first launch); zeroed by every solve's finalize.  Word 0 of
-    // set kGuardSets counts launches run in the SUMS form (diagnostics)
+    // kGuardSets spread sets (zeroed by every solve's finalize; r4's
+    // whole-solve SUMS guard used them), then the diagnostics words of set
+    // kGuardSets: [0] per-launch blocks run in the optimistic SUMS form, [1]
+    // chain launches, [2] waves / row groups re-run in the reference's form
     uint32_t *guard_slots;
 };
 
@@ -369,6 +369,9 @@ bool correct_head_ok(const Geom &g, const Fields &f);
 void launch_correct_head(const Geom &g, const Fields &f, int pass, float dt_override, bool has_next,
                          hipStream_t s);
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
+// Slabs with persistent runs (r5): copy this rank's abort word (persist[1],
+// a persistent solve timed out) into Ctl::red[6] before the step all-reduce
+void launch_abort_to_red(const Fields &f, hipStream_t s);
 
 // Jacobi kernel geometry (exported for the roofline bookkeeping in bench).
 constexpr int kJacRowsPerWave = 16;

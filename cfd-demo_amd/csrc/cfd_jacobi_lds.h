@@ -117,10 +117,12 @@ constexpr int ring_depth(int T, int PD, int G) {
 // overflow included; a subnormal h + v is exact).  k_jacobi_persist proves
 // that bound per task before it picks SUMS (its guard); otherwise, and for
 // every other launch, the reference's form runs.
-// GRD (r4, per-launch solves on a single domain, k_jacobi_lds): 2 = the
-// solve's first launch, tracks max |p'| of every input it loads (imax) and
-// max |rhs| (rmax) for the whole-solve SUMS guard; 1 = a later launch of the
-// solve (no tracking; lds_block decides its form from those two maxima).
+// GRD 3 (r5, the default per-launch form; it replaces r4's whole-solve guard
+// chain, GRD 1/2, which measured no faster than the reference's form): OPTIMISTIC SUMS -- the wave runs the
+// SUMS form while tracking max |p'| of every input row it loads (stage 1's
+// Tp, plus B and C at stage 1's first slot) and max |rhs|, then checks the
+// bound (lds_block); where it fails the wave re-runs its march in the
+// reference's form.
 template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1 || MODE == 5, SPEC = MODE == 2, REDO = MODE == 3;
@@ -136,7 +138,7 @@ struct LdsMarch {
 #ifndef CFD_PROBE_NOTRACK
 #define CFD_PROBE_NOTRACK 0   // (diagnostic builds: no guard tracking)
 #endif
-    static constexpr bool TRACK_IN = (PERSIST && !SUMS && !CFD_PROBE_NOTRACK) || GRD == 2;
+    static constexpr bool TRACK_IN = (PERSIST && !SUMS && !CFD_PROBE_NOTRACK) || GRD == 3;
     static constexpr bool TRACK_OUT = PERSIST && !CFD_PROBE_NOTRACK;
     static_assert(!SUMS || FAST == 1, "SUMS: reciprocal multiply");
     static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
@@ -319,6 +321,11 @@ struct LdsMarch {
                 if (s == 1) {
                     imax = fmaxf(fmaxf(imax, fabsf(Tp.x)), fabsf(Tp.y));
                     rmax = fmaxf(fmaxf(rmax, fabsf(rh.x)), fabsf(rh.y));
+                    // GRD 3: the wave's own bound also covers the first two
+                    // input rows (B and C of stage 1's first slot)
+                    if (GRD == 3 && GUARD == 0 && V_ == start(1))
+                        imax = fmaxf(fmaxf(imax, fmaxf(fabsf(B.x), fabsf(B.y))),
+                                     fmaxf(fabsf(C.x), fabsf(C.y)));
                 }
             }
             f2 n = stage<E>(B, C, Tp, rh);
@@ -465,20 +472,17 @@ struct LdsMarch {
 // trk (persistent blocks): per wave, trk[3 w .. 3 w + 2] = max |p'| of the
 // rows it stored, of the p' rows it loaded and of the rhs rows it used (the
 // last two only in the reference's form; 0 where not tracked or no rows).
-// The whole-solve SUMS guard of a per-launch single-domain solve.  M0 =
-// max |p'| the solve's first launch read (every cell of the source buffer;
-// the other buffer holds only values the solve itself stores), Rm = max
-// |rhs|.  A sweep moves max |p'| by at most 0.1875 Rm / R (|pu| <= M +
-// Rm / (4R), p_new = 0.75 pu + 0.25 p), so every value of the solve's
-// K = jacobi_iters sweeps stays below M0 + K 0.1875 Rm / R (rounding: a
-// factor 1 + 2^-12 at most over 512 sweeps); below plim = 2^124 / R every
-// h R, v R is < 2^126, the form's exactness bound.  NaN: max ignores it
-// and it propagates as the same operand in both forms; +-Inf fails.
-__device__ __forceinline__ bool sums_guard(float m0, float rm, float plim, float rlim, const Geom &g) {
-    // 0.1875 K Rm / R = 0.1875 K Rm dx^2 (FAST == 1 with R a power of two
-    // makes dx^2 exactly 1 / R)
-    const float drift = 0.1875f * (float)g.jacobi_iters * rm * g.dx_sq;
-    return m0 < 0.5f * plim && rm < rlim && drift < 0.5f * plim;
+// GRD 3 (the optimistic SUMS form, r5): a wave's T sweeps stay bitwise in
+// the form when every p' input it loads is below plim / 2 = 2^123 / R, every
+// rhs value below rlim = 2^124 and the drift T 0.1875 max|rhs| / R (a sweep
+// moves max |p'| by at most that: |pu| <= M + |rhs| / (4R), p_new = 0.75 pu
+// + 0.25 p) below plim / 2: then every h R, v R the sweeps form is < 2^126,
+// the form's exactness bound (see LdsMarch).  NaN: max ignores it and it
+// propagates as the same operand in either form; +-Inf fails the bound.
+__device__ __forceinline__ bool sums_bound(float im, float rm, float plim, float rlim, int T,
+                                           const Geom &g) {
+    const float drift = 0.1875f * (float)T * rm * g.dx_sq;   // dx^2 == 1 / R exactly (FAST 1)
+    return im < 0.5f * plim && rm < rlim && drift < 0.5f * plim;
 }
 
 template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
@@ -591,8 +595,8 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         w.PQ[q] = w.template ld<M::PLD_AUX>(w.rs_p, w.k_first + q);
         w.RQ[q] = w.ld(w.rs_r, w.k_first + q);
     }
-    // the march and what the launch publishes; `wx` is w, or (gprev) its
-    // SUMS-form twin (same members) when the chain guard allows it
+    // the march and what the launch publishes
+    bool redo = false;   // GRD 3: the bound failed, the reference's form re-runs the wave
     auto finish = [&](auto &wx) {
     using MX = typename std::remove_reference<decltype(wx)>::type;
     if (row_edge)
@@ -601,14 +605,10 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         wx.template run<MX::kCol>();
     else
         wx.template run<0>();
-    if constexpr (GRD == 2) {
-        // the whole-solve guard's inputs: max |p'| of what this first launch
-        // read and max |rhs|, one spread slot per wave
-        const float im = wave_max(wx.imax);
-        const float rm = wave_max(wx.rmax);
-        if (lane == 0) {
-            publish_max(gset, bid * kLdsWaves + wave, im);
-            publish_max(grhs, bid * kLdsWaves + wave, rm);
+    if constexpr (GRD == 3) {
+        if (!sums_bound(wave_max(wx.imax), wave_max(wx.rmax), plim, rlim, T, g)) {
+            redo = true;   // nothing published: the re-run does
+            return;
         }
     }
     if (M::PERSIST && trk) {
@@ -644,23 +644,16 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     const float m = wave_max(out_lane ? wx.m : 0.0f);
     if (lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, m);
     };
-    if constexpr (FAST == 1 && GRD == 1 && !SUMS && !M::PERSIST) {
-        if (gprev) {
-            // the whole-solve guard's two maxima, loaded while the prefetch is
-            // in flight (one global round trip for both)
-            const int gl = lane & (kResSlots - 1);
-            const float pin = wave_max(__uint_as_float(gprev[gl * kResStride]));
-            const float rin = wave_max(__uint_as_float(grhs[gl * kResStride]));
-            if (sums_guard(pin, rin, plim, rlim, g)) {
-                if (bid == 0 && threadIdx.x == 0)   // diagnostics: launches in the SUMS form
-                    atomicAdd(grhs + (size_t)kResSlots * kResStride, 1u);   // set kGuardSets
-                LdsMarch<T, FAST, MODE, true, GRD> w1(w);
-                finish(w1);
-                return;
-            }
+    finish(w);
+    if constexpr (GRD == 3) {
+        if (redo) {
+            // gset: the fallback counter (cfd_get_chain_stats)
+            if (lane == 0 && gset) atomicAdd(gset, 1u);
+            lds_block<T, FAST, MODE, false, 0>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc,
+                                               nseg, wlo, whi, lds, nst, bid, spec_fold, trk, nullptr,
+                                               nullptr, nullptr, plim, rlim, r0o, r1o);
         }
     }
-    finish(w);
 }
 
 // Minimum waves per SIMD the register allocation must allow (the SPEC
@@ -762,31 +755,16 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         par = ctl->spec_launch;   // re-run that launch: same source, same destination
     }
     if constexpr (FAST == 1 && (MODE == 0 || MODE == 1)) {
-        // The SUMS form on a guarded chain of launches (single domain; sums:
-        // the grid allows the form at all, see LdsMarch).  Launch g of the
-        // chain reads exactly what launch g-1 stored (every p' cell, boundary
-        // rows and columns included, is rewritten by every launch), so
-        // max |input| = launch g-1's published max |store|; the chain's
-        // first launch runs the reference's form and measures max |rhs| (rhs
-        // is constant in a solve).  Bounds as k_jacobi_persist's guard:
-        // inputs < plim = 2^124 / R and rhs < rlim = 2^124 keep every value
-        // the T sweeps form below 2^126 / R.  NaN propagates the same operand
-        // in either form (max is NaN-ignoring); +-Inf fails the guard.
-        const int gp = par - g.guard_par0;
-        if (sums && g.guard_par0 >= 0 && gp >= 0) {
+        // the optimistic SUMS form (GRD 3, r5; sums: the grid allows the form
+        // at all, see LdsMarch): every wave checks its own bound after its
+        // march and re-runs in the reference's form where it fails
+        if (sums) {
             constexpr size_t kSet = (size_t)kResSlots * kResStride;
-            uint32_t *const gin = gslots, *const grh = gslots + 4 * kSet;   // sets 0 and 4
-            const int bid = xcd_block(g);
-            if (gp == 0) {
-                lds_block<T, FAST, MODE, false, 2>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
-                                                   nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
-                                                   nullptr, gin, grh);
-            } else {
-                // the guard is decided inside (lds_block: its loads overlap the prefetch)
-                lds_block<T, FAST, MODE, false, 1>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi,
-                                                   nwc, nseg, wlo, whi, lds, nst, bid, spec_fold,
-                                                   nullptr, nullptr, grh, gin, plim, rlim);
-            }
+            uint32_t *const cnt = gslots ? gslots + kGuardSets * kSet : nullptr;   // [0] launches, [2] re-runs
+            if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(cnt, 1u);
+            lds_block<T, FAST, MODE, true, 3>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc,
+                                              nseg, wlo, whi, lds, nst, xcd_block(g), spec_fold, nullptr,
+                                              cnt ? cnt + 2 : nullptr, nullptr, nullptr, plim, rlim);
             return;
         }
     }
@@ -1213,20 +1191,17 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
     const int spec_fold = MODE == 2 && spec_fold_on() ? 1 : 0;
-    // the guarded SUMS form (k_jacobi_lds): reciprocal multiply, dx^2 ==
-    // dy^2 with a power-of-two reciprocal R >= 1, single domain, a chain set
-    // up by the host (Geom::guard_par0).  Opt-in here (CFD_JACOBI_SUMS=1):
-    // with the guard in, the per-launch march measured no faster (4096^2
-    // 5.09 vs 5.03 us per sweep, C3 11.46 vs 11.19 ms, ab_*_r4p.log; the
-    // unguarded probe 4.92 vs 5.09, ab_4096_r4m.log)
+    // the optimistic SUMS form (GRD 3): reciprocal multiply, dx^2 == dy^2
+    // with a power-of-two reciprocal R >= 1 (h R, v R exact below overflow),
+    // fixed-count launches; CFD_JACOBI_SUMS=0 keeps the reference's form.
+    // Read per launch (tests switch it).
     int sums = 0;
     float plim = 0.0f, rlim = 0.0f;
-    if ((MODE == 0 || MODE == 1) && g.guard_par0 >= 0 && g.fastdiv == 1 &&
-        g.j0 == 0 && g.nyl == g.ny && g.dx_sq == g.dy_sq && g.r_dx_sq == g.r_dy_sq) {
+    if ((MODE == 0 || MODE == 1) && g.fastdiv == 1 && g.dx_sq == g.dy_sq && g.r_dx_sq == g.r_dy_sq) {
         const char *ue = getenv("CFD_JACOBI_SUMS");
         int e2 = 0;
         const float R = g.r_dx_sq;
-        if (ue && atoi(ue) == 1 && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
+        if (!(ue && atoi(ue) == 0) && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
             sums = 1;
             plim = std::ldexp(1.0f, 124) / R;
             rlim = std::ldexp(1.0f, 124);

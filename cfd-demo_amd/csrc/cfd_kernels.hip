@@ -1196,6 +1196,20 @@ __device__ __forceinline__ void step_finalize_body(const Geom &g, const Fields &
     // maxima (a sharded fixed-count step skips the solve's own all-reduce)
     c->last_p = __uint_as_float(ld_ctl(&c->red[5]));
     c->red[0] = c->red[1] = c->red[2] = c->red[3] = c->red[4] = c->red[5] = 0u;
+    // a persistent solve on some slab timed out this step (all-reduced,
+    // launch_abort_to_red): every rank's host sees CFD_ETIMEOUT at its next
+    // synchronisation and all of them re-run from their checkpoints
+    // (cfd_model::recover); later persistent launches of this rank leave at once
+    if (ld_ctl(&c->red[6])) {
+        if (f.persist) __hip_atomic_store(f.persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f.host_nonfinite)
+            __hip_atomic_store(f.host_nonfinite + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ void k_abort_to_red(Fields f) {
+    if (threadIdx.x == 0 && f.persist)
+        f.ctl->red[6] = __hip_atomic_load(f.persist + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
 }
 
 __global__ void k_step_finalize(Geom g, Fields f) { step_finalize_body<false>(g, f); }
@@ -1803,6 +1817,10 @@ void launch_boundary(const Geom &g, const Fields &f, hipStream_t s) {
 void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s) {
     const size_t n = (size_t)(g.nyl + 1) * (g.nx + 1);
     hipLaunchKernelGGL(k_step_reduce, dim3(copy_grid(n / 4 + 1)), dim3(kBlock), 0, s, g, f);
+}
+
+void launch_abort_to_red(const Fields &f, hipStream_t s) {
+    hipLaunchKernelGGL(k_abort_to_red, dim3(1), dim3(64), 0, s, f);
 }
 
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s) {

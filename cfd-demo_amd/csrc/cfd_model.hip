@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/cfd.h"
@@ -1086,6 +1087,7 @@ struct cfd_model {
         }
         if (!launch_jacobi_persist(g, f, pass, par0, nblk, lo, hi, persist_epoch + 1, res_it, stream))
             return 0;
+        last_abort_resident = false;
         gate.last = stream;
         ++persist_epoch;
         *done = true;
@@ -1128,6 +1130,7 @@ struct cfd_model {
                 resident = launch_jacobi_resident(g, f, pass, iters, 1, pass >= 1 ? 1 : 0, stream);
                 if (resident) {
                     ++resident_solves;
+                    last_abort_resident = true;
                     gate.last = stream;
                     // launches the per-launch path would count (host_cur is
                     // not tracked with the tolerance on; Ctl::spec_launches is)
@@ -1145,7 +1148,6 @@ struct cfd_model {
                 // launch runs kSpecT sweeps with every sweep's residual, a check
                 // finds the reference's early exit (model.rs:816), and the
                 // converged launch is re-run with exactly its sweeps
-                g.guard_par0 = 0;   // one guarded chain (k_jacobi_lds's SUMS form)
                 for (int it = 0; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
@@ -1156,7 +1158,6 @@ struct cfd_model {
                     it += T;
                     ++launches;
                 }
-                g.guard_par0 = -1;
                 if (iters > 0) launch_jacobi_redo(g, f, pass, lo_g, hi_g, stream);
             } else if (tmax <= 1) {
                 for (int it = 0; it < iters; ++it)
@@ -1191,9 +1192,6 @@ struct cfd_model {
                         launches = nblk;
                     }
                 }
-                // the per-launch blocks form one guarded chain (the SUMS
-                // form's guard, k_jacobi_lds) from the first of them
-                g.guard_par0 = launches;
                 for (; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, tmax, iters, &T, &lo, &hi, &exch);
@@ -1202,7 +1200,6 @@ struct cfd_model {
                     it += T;
                     ++launches;
                 }
-                g.guard_par0 = -1;
             }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
         } else {
@@ -1654,7 +1651,10 @@ struct cfd_model {
         if (rc) return rc;
         if (!fused) launch_step_reduce(g, f, stream);
         if (sharded()) launch_fold_slots(f.ctl->red, f.red_slots, 4, stream);
-        rc = allreduce_max_u32(f.ctl->red, 6);   // maxima, non-finite flag, solve residual
+        // slabs with persistent runs: a rank whose persistent solve timed out
+        // tells every rank through the step all-reduce (red[6])
+        if (sharded() && persist_env && persist_sharded_env) launch_abort_to_red(f, stream);
+        rc = allreduce_max_u32(f.ctl->red, 7);   // maxima, non-finite flag, solve residual, abort
         if (rc) return rc;
         if (!step_finalize_folded) launch_step_finalize(g, f, stream);
         HIP_TRY(hipGetLastError());
@@ -1730,18 +1730,137 @@ struct cfd_model {
         HIP_TRY(hipSetDevice(device));
         int rc = wait_done(nullptr);
         if (rc) return rc;
-        return persist_timeout_check();
+        rc = persist_timeout_check(true);
+        if (rc) return rc;
+        ck_commit();   // everything enqueued so far is final: no replay needed
+        return 0;
     }
-    // a persistent solve that gave up waiting (k_jacobi_persist) left an
-    // invalid p': report it once and solve per launch from then on
-    int persist_timeout_check() {
+    // A persistent (k_jacobi_persist) or resident (k_jacobi_resident) solve
+    // that gave up waiting left an invalid p' and every step after it
+    // computed from it.  r5: the model recovers by itself -- it restores the
+    // checkpoint it took before the first entry since its last
+    // synchronisation (ck_begin) and re-runs those entries with one launch
+    // per block -- and reports the fault once (CFD_ETIMEOUT; the state is
+    // valid when it returns).  Solves run per launch from then on.
+    // at_sync: the stream has drained (slabs detect only there, so every rank
+    // re-runs the same entries)
+    int persist_timeout_check(bool at_sync) {
         if (!h_nonfinite || !*(volatile uint32_t *)(h_nonfinite + 2)) return 0;
+        if (!at_sync && sharded()) return 0;
+        const char *which = last_abort_resident ? "resident tolerance-mode" : "persistent";
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (cstream) HIP_TRY(hipStreamSynchronize(cstream));
         *(volatile uint32_t *)(h_nonfinite + 2) = 0u;
         persist_env = false;
         resident_off = true;
-        return fail(CFD_ETIMEOUT, "persistent Jacobi solve timed out waiting for a neighbouring "
-                                  "workgroup (not all resident); its result is invalid; "
+        if (ck_open) {
+            const size_t n_entries = ck_replay.size();
+            int rc = recover();
+            if (rc) return rc;
+            return fail(CFD_ETIMEOUT, std::string(which) + " Jacobi solve timed out waiting for a "
+                                      "workgroup; recovered: the state was restored from the "
+                                      "model's checkpoint and " + std::to_string(n_entries) +
+                                      " call(s) re-run with one launch per block (the state is "
+                                      "valid); per-launch solves from now on");
+        }
+        clear_abort_words();
+        return fail(CFD_ETIMEOUT, std::string(which) + " Jacobi solve timed out waiting for a "
+                                  "workgroup (no checkpoint was open); its result is invalid; "
                                   "per-launch solves from now on");
+    }
+
+    // ---- self-recovery checkpoint (r5) ---------------------------------
+    // Taken (stream-ordered device copies) at the first cfd_update_n /
+    // cfd_pressure_solve / cfd_piso_step after a synchronisation, when the
+    // model may run a persistent or resident solve; the entries enqueued
+    // since are kept as replays.  A synchronisation that finds no fault
+    // commits (drops) them.
+    struct CkSeg {
+        void *ptr;
+        size_t bytes;
+    };
+    std::vector<CkSeg> ck_segs;   // u, v, u_old, v_old, u*, v*, p, rhs, p' x2, Ctl
+    char *ck_pool = nullptr;
+    size_t ck_bytes = 0;
+    bool ck_open = false;
+    int ck_host_cur = 0;
+    bool ck_shallow = false;
+    std::vector<std::function<int()>> ck_replay;
+    uint64_t recoveries = 0;   // cfd_get_recoveries
+    bool last_abort_resident = false;
+    bool ckpt_env = [] {   // CFD_CKPT=0: no checkpoint (a timeout then invalidates the state)
+        const char *e = getenv("CFD_CKPT");
+        return !(e && atoi(e) == 0);
+    }();
+    bool ckpt_needed() const {
+        if (!ckpt_env || params.pressure_solver != CFD_SOLVER_JACOBI) return false;
+        if (persist_env && (sharded() ? persist_sharded_env : persist_req > 0)) return true;
+        return resident_mode();
+    }
+    int ck_begin() {
+        if (ck_open || !ckpt_needed()) return 0;
+        if (!ck_pool) {
+            size_t tot = 0;
+            for (const CkSeg &sg : ck_segs) tot += (sg.bytes + 255) & ~(size_t)255;
+            HIP_TRY(hipMalloc((void **)&ck_pool, tot));
+            ck_bytes = tot;
+        }
+        size_t off = 0;
+        for (const CkSeg &sg : ck_segs) {
+            HIP_TRY(hipMemcpyAsync(ck_pool + off, sg.ptr, sg.bytes, hipMemcpyDeviceToDevice, stream));
+            off += (sg.bytes + 255) & ~(size_t)255;
+        }
+        ck_host_cur = host_cur;
+        ck_shallow = pp_ghosts_shallow;
+        ck_replay.clear();
+        ck_open = true;
+        return 0;
+    }
+    void ck_record(std::function<int()> fn) {
+        if (ck_open) ck_replay.push_back(std::move(fn));
+    }
+    void ck_commit() {
+        ck_open = false;
+        ck_replay.clear();
+    }
+    // the abort word and the resident solve's barrier lines (its counters,
+    // generations and exit ticket stay where an aborted launch left them)
+    int clear_abort_words() {
+        HIP_TRY(hipMemset(f.persist, 0, (size_t)kPersistHeadLines * kPersistFlagStride * 4));
+        return 0;
+    }
+    int recover() {
+        size_t off = 0;
+        for (const CkSeg &sg : ck_segs) {
+            HIP_TRY(hipMemcpy(sg.ptr, ck_pool + off, sg.bytes, hipMemcpyDeviceToDevice));
+            off += (sg.bytes + 255) & ~(size_t)255;
+        }
+        // residual slot sets are zero between solves; an aborted solve may
+        // have left some behind
+        HIP_TRY(hipMemset(f.err_slots, 0, (size_t)kMaxSweeps * kResSlots * kResStride * 4));
+        int rc = clear_abort_words();
+        if (rc) return rc;
+        *(volatile uint32_t *)h_nonfinite = 0u;
+        host_cur = ck_host_cur;
+        pp_ghosts_shallow = ck_shallow;
+        fin_pending = false;
+        ++recoveries;
+        std::vector<std::function<int()>> replay;
+        replay.swap(ck_replay);
+        ck_open = false;
+        const bool tm = timing;
+        timing = false;   // the re-run is not a measurement
+        for (auto &fn : replay) {
+            rc = fn();
+            if (rc) break;
+        }
+        timing = tm;
+        if (rc) return rc;
+        rc = wait_done(nullptr);
+        if (rc) return rc;
+        if (*(volatile uint32_t *)(h_nonfinite + 2))   // per-launch solves cannot time out
+            return fail(CFD_ETIMEOUT, "the re-run after a solve timeout timed out");
+        return 0;
     }
 
     int read_ctl(Ctl *out) {
@@ -1771,6 +1890,7 @@ struct cfd_model {
                           (void *)mg_pool, (void *)mg_dev})
             if (ptr) (void)hipFree(ptr);
         if (h_nonfinite) (void)hipHostFree(h_nonfinite);
+        if (ck_pool) (void)hipFree(ck_pool);
         drop_graph();
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         if (ev_step0) (void)hipEventDestroy(ev_step0);
@@ -1964,7 +2084,6 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     // 7.3e11 vs 6.1e11 cell-updates/s at T = 8).  Single domain and slabs alike.
     g.tb_kind = g.fastdiv == 1 ? 5 : 4;
     g.pred_div = 2;
-    g.guard_par0 = -1;
     if (const char *e = getenv("CFD_PRED_DIV")) g.pred_div = std::min(std::max(atoi(e), 0), 2);
     if (const char *kv = getenv("CFD_TB_KIND")) {
         const int k = atoi(kv);
@@ -2030,6 +2149,11 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
         (rc = zalloc((void **)&m->ctl, sizeof(Ctl))) ||
         (rc = zalloc((void **)&m->slots, kSlotWords * 4)))
         return rc;
+    // the self-recovery checkpoint's segments (cfd_model::ck_begin)
+    m->ck_segs = {{m->u_all, u_alloc * 4}, {m->v_all, v_alloc * 4}, {m->uo_all, u_alloc * 4},
+                  {m->vo_all, v_alloc * 4}, {m->us_all, u_alloc * 4}, {m->vs_all, v_alloc * 4},
+                  {m->p, p_n * 4},         {m->rhs, pp_n * 4},        {m->pp_all[0], pp_n * 4},
+                  {m->pp_all[1], pp_n * 4}, {m->ctl, sizeof(Ctl)}};
     // word 0: first non-finite step; word 1: last finished step (watchdog)
     // [0] non-finite step, [1] progress (sharded), [2] persistent-solve timeout
     HIP_TRY(hipHostMalloc((void **)&m->h_nonfinite, 16, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2376,13 +2500,21 @@ int cfd_update(cfd_model *m) { return cfd_update_n(m, 1); }
 int cfd_update_n(cfd_model *m, int n) {
     if (!m) return fail(CFD_EINVAL, "null model");
     HIP_TRY(hipSetDevice(m->device));
+    // a solve timeout first (its junk steps may have raised the non-finite
+    // flag too): recovered from the checkpoint, reported once
+    if (int rc = m->persist_timeout_check(false)) return rc;
     // failure detection: a step the device has already finished left a NaN or
     // Inf in u/v (zero-copy word, no stream synchronisation)
     if (const uint32_t bad = *(volatile uint32_t *)m->h_nonfinite)
         return fail(CFD_ENONFINITE, "non-finite velocity (NaN/Inf) after step " + std::to_string(bad) +
                                         "; cfd_set_state clears it");
-    if (int rc = m->persist_timeout_check()) return rc;
     if (n <= 0) return 0;
+    if (int rc = m->ck_begin()) return rc;
+    m->ck_record([m, n]() {
+        for (int k = 0; k < n; ++k)
+            if (int rc = m->enqueue_update(k == n - 1)) return rc;
+        return 0;
+    });
     // solve timing: one event pair around the whole batch for the step time
     if (m->timing) {
         hipEvent_t e0 = m->take_event();
@@ -2406,6 +2538,11 @@ int cfd_update_n(cfd_model *m, int n) {
 int cfd_piso_step(cfd_model *m, float dt_sub) {
     if (!m) return fail(CFD_EINVAL, "null model");
     HIP_TRY(hipSetDevice(m->device));
+    if (int rc = m->ck_begin()) return rc;
+    m->ck_record([m, dt_sub]() {
+        int rc = m->exchange_uv();
+        return rc ? rc : m->enqueue_piso(dt_sub);
+    });
     int rc = m->exchange_uv();
     if (rc) return rc;
     return m->enqueue_piso(dt_sub);
@@ -2418,6 +2555,8 @@ int cfd_pressure_solve(cfd_model *m, float *residual_out) {
     if (m->host_driven()) {
         return m->enqueue_solve_host_driven(residual_out);
     }
+    if ((rc = m->ck_begin())) return rc;
+    m->ck_record([m]() { return m->enqueue_solve(-1); });
     rc = m->enqueue_solve(-1);
     if (rc) return rc;
     Ctl c;
@@ -2617,6 +2756,9 @@ int cfd_set_state(cfd_model *m, const cfd_state *st) {
     c.sweeps_total = st->jacobi_sweeps_total;
     c.nonfinite_step = 0;   // a new state: failure detection starts over
     c.red[4] = 0;
+    c.red[6] = 0;           // and an old solve timeout with it
+    rc = m->clear_abort_words();
+    if (rc) return rc;
     HIP_TRY(hipMemcpy(m->f.ctl, &c, offsetof(Ctl, go), hipMemcpyHostToDevice));
     *(volatile uint32_t *)m->h_nonfinite = 0u;
     m->host_cur = c.cur;
@@ -2828,6 +2970,12 @@ int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks) {
                       hipMemcpyDeviceToHost));
     if (launches) *launches = w[1];
     if (fallbacks) *fallbacks = w[2];
+    return 0;
+}
+
+int cfd_get_recoveries(const cfd_model *m, uint64_t *n) {
+    if (!m || !n) return fail(CFD_EINVAL, "null argument");
+    *n = m->recoveries;
     return 0;
 }
 

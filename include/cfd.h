@@ -49,14 +49,27 @@ typedef enum {
                             the reference has none): cfd_update refuses to step on
                             and cfd_get_residuals reports it (filling *out all the
                             same) until cfd_set_state injects a new state */
-    CFD_ETIMEOUT = -6, /* a persistent Jacobi solve (CFD_PERSIST=1) waited past its
-                          deadline (CFD_PERSIST_DEADLINE_US, default 10 s) for a
-                          neighbouring tile: a fault, not a residency effect (since r4
-                          the ticketed launch completes with any number of its
-                          workgroups resident, beside any other kernel).  That solve's
-                          p', and the steps enqueued after it, are invalid: restore a
-                          checkpoint (cfd_get_state / cfd_set_state); the model runs
-                          its solves one launch per block from then on */
+    CFD_ETIMEOUT = -6, /* a persistent Jacobi solve (k_jacobi_persist: CFD_PERSIST=1,
+                          or slabs with CFD_PERSIST_SHARDED=1) or the resident
+                          tolerance-mode solve (k_jacobi_resident: small single-domain
+                          grids by default) waited past its deadline
+                          (CFD_PERSIST_DEADLINE_US, default 10 s).  For the persistent
+                          solve that is a fault (it completes with any number of its
+                          workgroups resident); the resident solve needs all its
+                          workgroups co-resident, so co-tenant kernels that hold CUs for
+                          seconds can cause it.  Self-recovering since r5: the model
+                          checkpoints its state (device copies) before the first
+                          cfd_update_n / cfd_pressure_solve / cfd_piso_step after a
+                          synchronisation whenever such a solve may run; the call that
+                          detects the timeout (a synchronising call, or the next
+                          cfd_update_n on a single domain) restores that checkpoint,
+                          re-runs every call since with one launch per block, and
+                          returns CFD_ETIMEOUT with the state VALID (that detecting
+                          cfd_update_n itself enqueued nothing).  Slabs tell each
+                          other through the step all-reduce and recover at the same
+                          synchronisation.  Solves run per launch from then on;
+                          cfd_get_recoveries counts these.  CFD_CKPT=0 disables the
+                          checkpoint: the state is then invalid until cfd_set_state */
 } cfd_status;
 
 typedef struct cfd_model cfd_model;
@@ -251,17 +264,22 @@ int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
 /* 8-sweep blocks run in the SUMS form -- (h + v) / dx^2 for h / dx^2 +
  * v / dy^2, one instruction per column pair and sweep fewer, taken only where
  * a guard proves it bitwise: persistent-solve blocks per tile
- * (k_jacobi_persist's per-task guard) plus per-launch blocks (k_jacobi_lds's
- * chain guard) -- summed over the model's life.  Synchronises.  (new;
+ * (k_jacobi_persist's per-task guard) plus per-launch blocks (k_jacobi_lds,
+ * r5: the optimistic form -- every wave checks its own bound after its march
+ * and re-runs in the reference's form where it fails, cfd_get_chain_stats
+ * counts those) -- summed over the model's life.  Synchronises.  (new;
  * diagnostics) */
 int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
 /* The chained 8-sweep march (k_jacobi_chain, r5: a workgroup's four wave
  * segments hand their boundary rows to each other instead of recomputing
  * warm-up cones; opt-in CFD_JACOBI_CHAIN=1 for single-domain fixed-count
- * solves where its plan fits): launches run, and row groups whose optimistic SUMS form failed
- * its guard and were re-run in the reference's form, summed over the model's
+ * solves where its plan fits): chain launches run, and the chain row groups
+ * or per-launch waves (k_jacobi_lds) whose optimistic SUMS form failed its
+ * bound and were re-run in the reference's form, summed over the model's
  * life.  Synchronises.  (new; diagnostics) */
 int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks);
+/* Solve timeouts this model recovered from by itself (CFD_ETIMEOUT). */
+int cfd_get_recoveries(const cfd_model *m, uint64_t *n);
 /* Tolerance-mode solves this model enqueued as one resident launch
  * (k_jacobi_resident, see cfd_get_jacobi_kernel kind 6); diagnostics. */
 int cfd_get_resident_solves(const cfd_model *m, uint64_t *solves);

@@ -208,10 +208,12 @@ def test_persist_two_models_at_once(monkeypatch):
 
 def test_persist_deadline_fault_is_loud_and_recoverable(monkeypatch):
     """A wait past the deadline (forced here: CFD_PERSIST_DEADLINE_US=0, so
-    any neighbour not yet done counts as a fault) aborts the launch: the next
-    call raises CFD_ETIMEOUT, the model's later solves run per launch, and the
-    caller's checkpoint (cfd_get_state / cfd_set_state) restores a state from
-    which the steps equal the oracle."""
+    any neighbour not yet done counts as a fault) aborts the launch.  r5: the
+    model recovers by itself -- the synchronisation that sees the fault
+    restores the checkpoint the model took after its last synchronisation
+    and re-runs the steps since with one launch per block -- and reports it
+    once (CFD_ETIMEOUT).  With NO set_state by the caller, every later step
+    equals the oracle, and the model's solves run per launch from then on."""
     import cfdamd
     from cfdamd._lib import CFD_ETIMEOUT, CfdError
     from oracle import OracleModel
@@ -225,15 +227,22 @@ def test_persist_deadline_fault_is_loud_and_recoverable(monkeypatch):
         for _ in range(3):
             m.update()
             o.update()
-        ckpt = m.get_state()
         monkeypatch.setenv("CFD_PERSIST_DEADLINE_US", "0")
+        steps = 0   # updates the model accepted
         with pytest.raises(CfdError) as ei:
             for _ in range(20):   # a fault on the first persistent solve is near-certain
                 m.update()
+                steps += 1
                 m.synchronize()
         assert ei.value.code == CFD_ETIMEOUT, ei.value
+        assert "recovered" in str(ei.value), ei.value
+        assert m.recoveries == 1
         monkeypatch.delenv("CFD_PERSIST_DEADLINE_US")
-        m.set_state(**ckpt)
+        for _ in range(steps):
+            o.update()
+        st = m.get_state()
+        for f in STATE:
+            assert_bitwise(f"recovered state:{f}", st[f], o.field(f))
         for _ in range(2):
             m.update()
             o.update()
@@ -244,6 +253,97 @@ def test_persist_deadline_fault_is_loud_and_recoverable(monkeypatch):
     finally:
         m.close()
 
+
+def test_persist_deadline_fault_recovers_batched_steps(monkeypatch):
+    """The same fault inside a cfd_update_n batch of 4 steps: the batch is
+    re-run whole from the checkpoint (taken at its start) and equals the
+    oracle's 4 steps."""
+    import cfdamd
+    from cfdamd._lib import CFD_ETIMEOUT, CfdError
+    from oracle import OracleModel
+    grid = pow2_grid(512, 384)
+    params = cfdamd.SimulationParams.cavity(400.0, 64, corrector_passes=0, tol_enabled=False)
+    o = OracleModel(grid.nx, grid.ny, grid.lx, grid.ly, bc_kind=1, viscosity=1.0 / 400.0,
+                    jacobi_iters=64, tol_enabled=False, corrector_passes=0)
+    monkeypatch.setenv("CFD_PERSIST", "1")
+    m = cfdamd.Model(grid, params, device=0)
+    try:
+        m.update_n(2)
+        m.synchronize()
+        for _ in range(2):
+            o.update()
+        monkeypatch.setenv("CFD_PERSIST_DEADLINE_US", "0")
+        m.update_n(4)
+        with pytest.raises(CfdError) as ei:
+            m.synchronize()
+        assert ei.value.code == CFD_ETIMEOUT and m.recoveries == 1, ei.value
+        monkeypatch.delenv("CFD_PERSIST_DEADLINE_US")
+        for _ in range(4):
+            o.update()
+        st = m.get_state()
+        for f in STATE:
+            assert_bitwise(f"batch recovered:{f}", st[f], o.field(f))
+    finally:
+        m.close()
+
+
+@pytest.mark.timeout(300)
+def test_persist_deadline_fault_on_slabs_recovers_every_rank(monkeypatch):
+    """Slabs with persistent runs (CFD_PERSIST_SHARDED=1) and a forced
+    deadline fault: the rank that timed out tells the others through the
+    step all-reduce (Ctl::red[6]), every rank recovers at the same
+    synchronisation and re-runs the same steps, and the slabs equal the
+    single-domain per-launch model bit for bit."""
+    import threading
+    import cfdamd
+    from cfdamd._lib import CFD_ETIMEOUT, CfdError
+    n = 2
+    grid = cfdamd.cavity_grid(512, 1024)
+    params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
+    ref = cfdamd.Model(grid, params, device=0)
+    try:
+        ref.update_n(5)
+        want = ref.get_state()
+    finally:
+        ref.close()
+    monkeypatch.setenv("CFD_HALO_DEPTH", "32")
+    monkeypatch.setenv("CFD_PERSIST_SHARDED", "1")
+    hub = cfdamd.LocalHub(n)
+    out, codes, models, errors = [None] * n, [None] * n, [None] * n, []
+
+    def worker(r):
+        try:
+            m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=r, local_hub=hub)
+            models[r] = m
+            m.update_n(5)
+            try:
+                m.synchronize()
+                codes[r] = 0
+            except CfdError as e:
+                codes[r] = e.code
+            out[r] = (m.get_state(), m.j0, m.j1, m.recoveries)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    monkeypatch.setenv("CFD_PERSIST_DEADLINE_US", "0")   # every wait faults
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(240)
+    for m in models:
+        if m is not None:
+            m.close()
+    hub.close()
+    if errors:
+        raise errors[0]
+    assert codes == [CFD_ETIMEOUT] * n, codes
+    nx = grid.nx
+    for st, j0, j1, rec in out:
+        assert rec == 1
+        for f in ("p_prime", "p", "rhs"):
+            assert_bitwise(f"slab recovered {j0}:{f}", st[f], want[f].reshape(-1, nx)[j0:j1].ravel())
+        assert_bitwise(f"slab recovered {j0}:u", st["u"], want["u"].reshape(-1, nx + 1)[j0:j1].ravel())
 
 def test_persist_off_under_graph_replay(monkeypatch):
     """CFD_GRAPH=1 replays captured steps with frozen kernel arguments, so
@@ -351,10 +451,9 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     and the per-task guard falls back to the reference's form where a task
     reads a huge value: p' = 2^110 in one corner (the tiles there and those
     its values reach), rhs = 2^126 (> the 2^124 limit) in one patch (the
-    tiles that read it); distant tiles keep SUMS.  The per-launch march's
-    chain guard (k_jacobi_lds, r4: global maxima, the solve's first launch
-    exact) takes SUMS on launches 1..24 of the plain case and none where a
-    huge value sits anywhere.  Every case bitwise vs per-launch solves in the
+    tiles that read it); distant tiles keep SUMS.  The per-launch march
+    (k_jacobi_lds, r5: the optimistic form, each wave checks its own bound
+    after its march) re-runs exactly the waves that read a huge value.  Every case bitwise vs per-launch solves in the
     reference's form (CFD_PERSIST=0, CFD_JACOBI_SUMS=0)."""
     import cfdamd
     grid = cfdamd.cavity_grid(1024)
@@ -381,6 +480,7 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     per_launch_sums = {}
     sums = {}
     chain_fb = {}
+    lds_fb = {}
     for name, inject in cases.items():
         out = {}
         for key, env in envs.items():
@@ -395,6 +495,8 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
                     cs = mm.chain_stats
                     assert cs["launches"] == 25, cs
                     chain_fb[name] = cs["fallbacks"]
+                if key == "per_launch_sums":
+                    lds_fb[name] = mm.chain_stats["fallbacks"]
             finally:
                 mm.close()
         for key, (pp, _, _) in out.items():
@@ -403,9 +505,11 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
         assert out["per_launch"][1:] == (0, 0), out["per_launch"][1:]
         sums[name] = out["sums"][2]
         per_launch_sums[name] = out["per_launch_sums"][2]
-    # per-launch chain (k_jacobi_lds, global guard): launches 1..24 of the 25
-    # in the SUMS form; a huge p' or rhs anywhere keeps every launch exact
-    assert per_launch_sums == {"plain": 24, "huge_pp": 0, "huge_rhs": 0}, per_launch_sums
+    # per-launch march (k_jacobi_lds, r5: the optimistic form): all 25
+    # launches run it; the waves that read a huge value re-run in the
+    # reference's form, none in the plain case
+    assert per_launch_sums == {"plain": 25, "huge_pp": 25, "huge_rhs": 25}, per_launch_sums
+    assert lds_fb["plain"] == 0 and lds_fb["huge_pp"] > 0 and lds_fb["huge_rhs"] > 0, lds_fb
     # plain: the owned tiles' blocks 2..24 (blocks 0 and 1 measure the inputs)
     assert sums["plain"] > 0, sums
     assert 0 < sums["huge_pp"] < sums["plain"] and 0 < sums["huge_rhs"] < sums["plain"], sums

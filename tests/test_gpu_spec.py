@@ -212,9 +212,10 @@ def test_spec_fold_matches_check_launch(monkeypatch, p_tol):
 
 def test_resident_deadline_fault_is_loud_and_recoverable(monkeypatch):
     """A barrier wait past the deadline (forced: CFD_PERSIST_DEADLINE_US=0)
-    aborts the resident solve: the next call raises CFD_ETIMEOUT, the model's
-    later solves run per launch, and the caller's checkpoint restores a state
-    from which the steps equal the oracle, sweep counts included."""
+    aborts the resident solve.  r5: the model recovers by itself (checkpoint
+    restored, the steps since re-run per launch), reports it once
+    (CFD_ETIMEOUT), and with NO set_state by the caller every later step
+    equals the oracle, sweep counts included."""
     import cfdamd
     from cfdamd._lib import CFD_ETIMEOUT, CfdError
     from oracle import OracleModel
@@ -229,17 +230,22 @@ def test_resident_deadline_fault_is_loud_and_recoverable(monkeypatch):
             m.update()
             o.update()
             _compare(f"resident before fault {k}", m, o)
-        ckpt = m.get_state()
         monkeypatch.setenv("CFD_PERSIST_DEADLINE_US", "0")
         monkeypatch.setenv("CFD_PERSIST_LATE", "3")   # workgroups 1, 4, ... arrive 2 ms late
+        steps = 0
         with pytest.raises(CfdError) as ei:
             for _ in range(5):   # the first barrier wait faults
                 m.update()
+                steps += 1
                 m.synchronize()
         assert ei.value.code == CFD_ETIMEOUT, ei.value
+        assert "resident" in str(ei.value) and "recovered" in str(ei.value), ei.value
+        assert m.recoveries == 1
         monkeypatch.delenv("CFD_PERSIST_DEADLINE_US")
         monkeypatch.delenv("CFD_PERSIST_LATE")
-        m.set_state(**ckpt)
+        for k in range(steps):
+            o.update()
+        _compare("resident recovered", m, o)
         assert m.jacobi_kernel["kind"] == 5   # per launch after the fault
         for k in range(3):
             m.update()
