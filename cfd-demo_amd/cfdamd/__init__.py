@@ -467,6 +467,13 @@ class Model:
         return dict(launches=int(a.value), fallbacks=int(b.value))
 
     @property
+    def comm_calls(self) -> int:
+        """Halo-exchange groups + all-reduces enqueued (cfd_get_comm_calls)."""
+        n = C.c_uint64()
+        check("cfd_get_comm_calls", load().cfd_get_comm_calls(self._hh(), C.byref(n)))
+        return int(n.value)
+
+    @property
     def recoveries(self) -> int:
         """Solve timeouts the model recovered from by itself: checkpoint
         restored, calls since re-run per launch (cfd_get_recoveries)."""

@@ -152,6 +152,8 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
             const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
             // one buffer flip per launch: per sweep with the tolerance on,
             // `flips` (host-known launch count) for fixed-count solves
+            // 3 (r5, the speculative solve on slabs): `flips` launches, the
+            // converged launch's result aligned to that buffer (k_spec_align)
             c->cur = (c->cur + (exact_flips == 2 ? c->spec_launches
                                 : (g.tol_enabled && !exact_flips) ? n : flips)) & 1;
             c->last_p = res;
@@ -161,7 +163,7 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
         }
         if (pass >= 0 && pass + 1 <= kMaxPasses)
             c->go[pass + 1] = (go && !(check_break && g.tol_enabled && c->last_p < g.p_tol)) ? 1 : 0;
-        if (exact_flips == 2) c->spec_stop = c->spec_redo = c->spec_launch = c->spec_launches = 0;
+        if (exact_flips >= 2) c->spec_stop = c->spec_redo = c->spec_launch = c->spec_launches = 0;
         go_s = go;
     }
     __syncthreads();

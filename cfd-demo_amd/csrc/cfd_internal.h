@@ -254,6 +254,9 @@ void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, 
 bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, int fin,
                             int check_break, hipStream_t s);
 bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *wgs);
+// slabs (r5): after the re-run, the converged launch's result moved to the
+// buffer the host counts n launches ahead (k_spec_align; nyl * nx % 4 == 0)
+void launch_spec_align(const Geom &g, const Fields &f, int pass, int n, hipStream_t s);
 void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
                         hipStream_t s);
 // dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before

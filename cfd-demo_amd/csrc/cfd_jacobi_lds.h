@@ -729,6 +729,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
     const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
     struct StampOnExit {
         unsigned long long rt0, t0;
+        unsigned long long bid;   // the XCD-renumbered block (tile: bid % nwc, row group bid / nwc)
         __device__ ~StampOnExit() {
             if (RES) return;
             const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -740,11 +741,11 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
             if ((threadIdx.x & 63) == 0 && idx < kStampWaves) {
                 g_lds_stamp[idx * 4 + 0] = rt0;
                 g_lds_stamp[idx * 4 + 1] = rt1;
-                g_lds_stamp[idx * 4 + 2] = t1 - t0;
+                g_lds_stamp[idx * 4 + 2] = (bid << 40) | ((t1 - t0) & 0xFFFFFFFFFFull);
                 g_lds_stamp[idx * 4 + 3] = ((unsigned long long)xcc << 32) | hw;
             }
         }
-    } stamp_guard{st_rt0, st_t0};
+    } stamp_guard{st_rt0, st_t0, (unsigned long long)xcd_block(g)};
 #endif
     if (pass_off(ctl, pass)) return;
     if (M::SPEC && ctl->spec_stop) return;   // an earlier launch of the solve converged
@@ -1193,15 +1194,17 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int spec_fold = MODE == 2 && spec_fold_on() ? 1 : 0;
     // the optimistic SUMS form (GRD 3): reciprocal multiply, dx^2 == dy^2
     // with a power-of-two reciprocal R >= 1 (h R, v R exact below overflow),
-    // fixed-count launches; CFD_JACOBI_SUMS=0 keeps the reference's form.
-    // Read per launch (tests switch it).
+    // fixed-count launches.  Opt-in (CFD_JACOBI_SUMS=1): with its input
+    // tracking it measured slower than the reference's form, 5.03 vs 4.97 us
+    // per sweep at 4096^2 (profiles/r5/prof_r5f/ab_sums.log).  Read per launch
+    // (tests switch it).
     int sums = 0;
     float plim = 0.0f, rlim = 0.0f;
     if ((MODE == 0 || MODE == 1) && g.fastdiv == 1 && g.dx_sq == g.dy_sq && g.r_dx_sq == g.r_dy_sq) {
         const char *ue = getenv("CFD_JACOBI_SUMS");
         int e2 = 0;
         const float R = g.r_dx_sq;
-        if (!(ue && atoi(ue) == 0) && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
+        if (ue && atoi(ue) == 1 && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
             sums = 1;
             plim = std::ldexp(1.0f, 124) / R;
             rlim = std::ldexp(1.0f, 124);

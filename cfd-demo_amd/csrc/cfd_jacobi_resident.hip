@@ -47,6 +47,8 @@
 // group counters, 13-20: group generations); the workgroup that draws the
 // last exit ticket zeroes them, so every launch starts from 0.
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "cfd_device.h"
 
@@ -380,25 +382,54 @@ inline int resident_waves() {
     return e && atoi(e) == 16 ? 16 : 8;
 }
 
+inline int resident_rows() {
+    const char *re = getenv("CFD_RESIDENT_ROWS");
+    const int r = re ? atoi(re) : 2;
+    return r == 1 || r == 4 ? r : 2;
+}
+
+// Workgroups of the instantiation that will be launched (waves, rows per
+// thread) per CU with `lds` bytes of dynamic LDS; cached per (instantiation,
+// lds) -- the plan is consulted on every tolerance-mode solve
 template <int FAST>
 int resident_blocks_per_cu(int lds) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, int> cache;
+    const int waves = resident_waves(), rows = resident_rows();
+    const int key = waves * 16 + rows;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({key, lds});
+    if (it != cache.end()) return it->second;
+    const void *k = waves == 16 ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 16, 2>)
+                    : rows == 1 ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 1>)
+                    : rows == 4 ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 4>)
+                                : reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 2>);
     int n = 0;
-    const void *k = resident_waves() == 8
-                        ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 2>)
-                        : reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 16, 2>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, resident_waves() * 64, lds) != hipSuccess)
-        return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, waves * 64, lds) != hipSuccess) n = 0;
+    cache[{key, lds}] = n;
     return n;
 }
 
+// workgroups per CU the grid may use (CFD_RESIDENT_GPC, 1 or 2): 2 spreads
+// smaller tiles over twice the workgroups (two per CU, so every grid-barrier
+// wait has a second workgroup to hide behind); the launch is then taken only
+// where the occupancy query admits 3 per CU (a margin over the 2 it needs)
+inline int resident_gpc() {
+    const char *e = getenv("CFD_RESIDENT_GPC");
+    return e && atoi(e) == 2 ? 2 : 1;
+}
+
 // Tile shape: the candidate with the least LDS-box work per workgroup
-// (ceil(tiles / G) x box cells), every candidate admitting 2 workgroups per CU.
-// Single domain only (rows 0..ny-1 owned; the fields' ghost rows unused).
+// (ceil(tiles / G) x box cells), every candidate admitting 2 workgroups per CU
+// (gpc 1; 3 with gpc 2).  Single domain only (rows 0..ny-1 owned; the fields'
+// ghost rows unused).  The occupancy queries are cached; the rest is a few
+// integer operations.
 bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
     if (g.nx < 4 || g.ny < 4 || g.j0 != 0 || g.nyl != g.ny) return false;
     // box widths BC + 2e (e = 0..T-1) fill 64-lane passes: BC = 48 -> 48..62
     // columns in one pass, 112 -> 112..126 in two
     static const int cand[][2] = {{8, 48}, {16, 48}, {32, 48}, {16, 112}, {32, 112}};
+    const int gpc = resident_gpc();
     long best = -1;
     for (const auto &cd : cand) {
         int BR = cd[0], BC = cd[1];
@@ -411,10 +442,10 @@ bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
                         : g.res_div == 2 ? resident_blocks_per_cu<2>(lds)
                         : g.res_div == 3 ? resident_blocks_per_cu<3>(lds)
                                          : resident_blocks_per_cu<0>(lds);
-        if (occ < 2) continue;
+        if (occ < gpc + 1) continue;
         const int tx = cdiv(g.nx, BC), ty = cdiv(g.ny, BR);
         const long nt = (long)tx * ty;
-        const int G = (int)std::min<long>(nt, g.n_cu);
+        const int G = (int)std::min<long>(nt, (long)gpc * g.n_cu);
         const long work = (long)cdiv(nt, G) * (BR + 2 * T) * (BC + 2 * T);
         if (best < 0 || work < best) {
             best = work;
@@ -453,8 +484,7 @@ bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters,
     // the grid barrier: two-level (default) or one counter (CFD_RESIDENT_BAR=flat)
     const char *be = getenv("CFD_RESIDENT_BAR");
     const int xbar = be && strcmp(be, "flat") == 0 ? 0 : 1;
-    const char *re = getenv("CFD_RESIDENT_ROWS");
-    const int rows = re ? atoi(re) : 2;
+    const int rows = resident_rows();
 #define CFD_RES_LAUNCH(FASTV, WV, RW)                                                              \
     hipLaunchKernelGGL((k_jacobi_resident<FASTV, WV, RW>), dim3(p.G), dim3(WV * 64), p.lds, s, g, \
                        f, pass, iters, T, p.BR, p.BC, p.tiles_x, p.ntiles,                        \

@@ -708,6 +708,24 @@ __global__ __launch_bounds__(kBlock) void k_spec_check(Geom g, Fields f, int pas
     }
 }
 
+// The speculative solve on slabs (r5): the host counts every launch of the
+// solve as a buffer flip (it must know which buffer's ghost rows to exchange
+// before each launch), so when a launch L < n-1 converged and its re-run
+// left the result in buffer cur + L + 1 of the other parity, that buffer's
+// owned rows are copied to buffer cur + n (the ghost rows are re-exchanged
+// before they are read again).
+__global__ __launch_bounds__(kBlock) void k_spec_align(Geom g, Fields f, int pass, int n) {
+    const Ctl *c = f.ctl;
+    if (pass_off(c, pass) || !c->spec_stop) return;
+    const int L = c->spec_launch;
+    if (((n - (L + 1)) & 1) == 0) return;
+    const float4 *src = reinterpret_cast<const float4 *>(f.pp[(c->cur + L + 1) & 1]);
+    float4 *dst = reinterpret_cast<float4 *>(f.pp[(c->cur + n) & 1]);
+    const size_t n4 = (size_t)g.nyl * g.nx / 4;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 // dst[q] = max(dst[q], slots of set q), then zero the slots (q < n).
 __global__ void k_fold_slots(uint32_t *dst, uint32_t *slots, int n) {
     const int q = (int)threadIdx.x;
@@ -1677,6 +1695,10 @@ void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, in
                         hipStream_t s) {
     if (out_hi <= out_lo) return;
     launch_lds(g, f, kMaxTemporal, pass, 0, 0, out_lo, out_hi, nullptr, s, 3);
+}
+
+void launch_spec_align(const Geom &g, const Fields &f, int pass, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_spec_align, dim3(256), dim3(kBlock), 0, s, g, f, pass, n);
 }
 
 void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s) {

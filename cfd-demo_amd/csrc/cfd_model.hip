@@ -217,8 +217,10 @@ struct cfd_model {
 
     // Ghost-row exchange of one field with both neighbours (geometry from
     // plan_halo): one RCCL group of at most two sends and two receives.
+    uint64_t comm_calls = 0;   // halo groups + all-reduces enqueued (cfd_get_comm_calls)
     int exchange(int id, int kind, int depth, hipStream_t st = nullptr) {
         if (!sharded()) return 0;
+        ++comm_calls;
         if (!st) st = stream;
         if (hub) return exchange_local(id, kind, depth, st);
         if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
@@ -279,6 +281,7 @@ struct cfd_model {
     // ONE RCCL group (one launch latency over xGMI instead of two).
     int exchange_uv(hipStream_t st = nullptr) {
         if (!sharded()) return 0;
+        ++comm_calls;
         if (!st) st = stream;
         if (hub) {
             int rc = exchange_local(FLD_U, HALO_U, 2, st);
@@ -302,6 +305,7 @@ struct cfd_model {
 
     int allreduce_max_u32(uint32_t *dev, size_t n) {
         if (!sharded()) return 0;
+        ++comm_calls;
         if (hub) {
             std::vector<uint32_t> acc(n, 0u), mine(n);
             HIP_TRY(hipStreamSynchronize(stream));
@@ -1111,7 +1115,9 @@ struct cfd_model {
         int launches = 0;   // buffers flip once per launch
         bool resident = false;   // the resident launch also finalizes the solve
         if (!sharded()) {
-            if (spec && resident_mode()) {
+            // (never under hipGraph capture: its workgroups must be resident
+            // at once, and the device gate orders only eager launches)
+            if (spec && resident_mode() && !capturing) {
                 // the whole solve in one launch, the early exit decided on the
                 // device; in-process resident / persistent launches of
                 // different models on one device are ordered (all its
@@ -1202,6 +1208,15 @@ struct cfd_model {
                 }
             }
             if (evt) HIP_TRY(hipEventRecord(e1, stream));   // sweeps only
+        } else if (g.tol_enabled && spec_slab_ok()) {
+            const int n = enqueue_spec_slabs(pass, evt ? e1 : nullptr);
+            if (n < 0) return n;
+            if (evt) {
+                solve_events.emplace_back(e0, e1);
+                timed_sweeps += (uint64_t)iters;
+                timed_launches += (uint64_t)n;
+            }
+            return 0;
         } else {
             // the deep-halo sweeps recompute ghost rows, which read rhs there.
             // Overlapped (r2): the rhs exchange runs on cstream while the first
@@ -1423,7 +1438,58 @@ struct cfd_model {
         return 0;
     }
 
-    bool host_driven() const { return sharded() && params.tol_enabled; }
+    bool host_driven() const { return sharded() && params.tol_enabled && !spec_slab_ok(); }
+    // r5: the tolerance-mode Jacobi solve on slabs as speculative T-sweep
+    // blocks (enqueue_solve): per block one T-row p' exchange, one speculative
+    // launch publishing every sweep's residual, one all-reduce of the block's
+    // T residuals and the device-side check -- instead of a launch, a fold,
+    // an all-reduce, an exchange and a host read per sweep.  CFD_SPEC_SLABS=0
+    // keeps the host-driven per-sweep loop.
+    bool spec_slab_env = [] {
+        const char *e = getenv("CFD_SPEC_SLABS");
+        return !(e && atoi(e) == 0);
+    }();
+    bool spec_slab_ok() const {
+        return sharded() && spec_env && spec_slab_env && params.pressure_solver == CFD_SOLVER_JACOBI &&
+               g.hg >= 2 && g.nyl >= 2 * kMaxTemporal && ((size_t)g.nyl * g.nx) % 4 == 0;
+    }
+    int enqueue_spec_slabs(int pass, hipEvent_t e1) {
+        const int iters = params.jacobi_iters;
+        const int Tm = std::min(kMaxTemporal, g.hg);
+        const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
+        // every block reads rhs rows T deep into the ghosts
+        int rc = exchange(FLD_RHS, HALO_PP, g.hg);
+        if (rc) return rc;
+        const int nb = iters > 0 ? (iters + Tm - 1) / Tm : 0;
+        int it = 0, launches = 0;
+        for (int b = 0; b < nb; ++b) {
+            const int T = iters / nb + (b < iters % nb ? 1 : 0);   // even split, no short tail
+            rc = exchange_pp((host_cur + launches) & 1, T);         // the block's source, T rows deep
+            if (rc) return rc;
+            launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream);
+            launch_fold_slots(f.ctl->err + it, f.err_slots + (size_t)it * kResSlots * kResStride, T,
+                              stream);
+            rc = allreduce_max_u32(f.ctl->err + it, (size_t)T);   // every rank decides alike
+            if (rc) return rc;
+            launch_spec_check(g, f, pass, it, T, launches, stream);
+            it += T;
+            ++launches;
+        }
+        if (iters > 0) {
+            launch_jacobi_redo(g, f, pass, lo, hi, stream);
+            launch_spec_align(g, f, pass, launches, stream);
+            // the corrector reads one p' ghost row of the result (the re-run
+            // and the alignment wrote owned rows only)
+            rc = exchange_pp((host_cur + launches) & 1, 1);
+            if (rc) return rc;
+        }
+        if (e1) HIP_TRY(hipEventRecord(e1, stream));
+        launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream, 3);
+        HIP_TRY(hipGetLastError());
+        host_cur = (host_cur + launches) & 1;
+        pp_ghosts_shallow = true;   // the converged block's re-run: ghosts stale
+        return launches;
+    }
 
     // Persistent fixed-count solve (k_jacobi_persist); CFD_PERSIST=0 opts out
     // everywhere.  Each launch gets a new flag epoch from the host (flags start
@@ -2970,6 +3036,12 @@ int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks) {
                       hipMemcpyDeviceToHost));
     if (launches) *launches = w[1];
     if (fallbacks) *fallbacks = w[2];
+    return 0;
+}
+
+int cfd_get_comm_calls(const cfd_model *m, uint64_t *n) {
+    if (!m || !n) return fail(CFD_EINVAL, "null argument");
+    *n = m->comm_calls;
     return 0;
 }
 

@@ -278,6 +278,9 @@ int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
  * bound and were re-run in the reference's form, summed over the model's
  * life.  Synchronises.  (new; diagnostics) */
 int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks);
+/* Collective calls this (sharded) model has enqueued: halo-exchange groups
+ * and all-reduces, summed over its life (0 unsharded).  (new; diagnostics) */
+int cfd_get_comm_calls(const cfd_model *m, uint64_t *n);
 /* Solve timeouts this model recovered from by itself (CFD_ETIMEOUT). */
 int cfd_get_recoveries(const cfd_model *m, uint64_t *n);
 /* Tolerance-mode solves this model enqueued as one resident launch

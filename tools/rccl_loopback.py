@@ -100,9 +100,10 @@ def worker(args):
         st = m.get_state()
         mine = {k: st[k] for k in ("u", "v", "p", "p_prime")}
         slab = (m.j0, m.j1)
+        calls = m.comm_calls / max(1, args.steps)
         m.close()
         gathered = [None] * n
-        dist.all_gather_object(gathered, (slab, mine))
+        dist.all_gather_object(gathered, (slab, mine, calls))
         if rank == 0:
             ref = cfdamd.Model(grid, params, device=0)
             for _ in range(args.steps):
@@ -113,7 +114,7 @@ def worker(args):
             ok = True
             for k in ("u", "v", "p", "p_prime"):
                 parts = []
-                for i, ((j0, j1), f) in enumerate(gathered):
+                for i, ((j0, j1), f, _) in enumerate(gathered):
                     if k == "v":
                         rows = f[k].reshape(j1 - j0 + 1, nx)
                         parts.append(rows if i == n - 1 else rows[:-1])
@@ -124,7 +125,8 @@ def worker(args):
                 ok &= same
             report.append({"case": name, "ranks": n, "grid": [grid.nx, grid.ny],
                            "steps": args.steps, "bitwise_equal_single_domain": bool(ok),
-                           "sharded_wall_s": round(el, 3)})
+                           "sharded_wall_s": round(el, 3),
+                           "collective_calls_per_step_rank0": gathered[0][2]})
     if rank == 0:
         for r in report:
             result(args, rank, r)
