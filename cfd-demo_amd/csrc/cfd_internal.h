@@ -223,8 +223,11 @@ void launch_pipe2(const Geom &g, const Fields &f, int T, int pass, int it, int p
 // mode 2 / 3: the speculative launch / its re-run (launch_jacobi_spec)
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
                          int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s);
+// lag (r5, speculative solves on one domain): mode 2 -- the previous launch's
+// sweep count, whose early-exit check this launch makes (0: none); mode 3 --
+// the solve's last launch's, checked by the re-run (see k_jacobi_lds)
 void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
-                int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0);
+                int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0, int lag = 0);
 // r5: an 8-sweep block of a single-domain solve as the chained march
 // (cfd_jacobi_chain.hip: a workgroup's four wave segments hand their boundary
 // rows to each other instead of recomputing cones); false: its plan does not
@@ -244,8 +247,11 @@ bool chain_plan(const Geom &g, int out_lo, int out_hi, int occ, int *nwc, int *n
 // below p_tol and, when it is not the launch's last, schedules the re-run
 // (launch_jacobi_redo) of that launch with exactly that many sweeps from its
 // untouched source buffer.  Later launches of the solve return at once.
+// lag > 0 (r5, one domain): no k_spec_check launches -- each launch checks the
+// previous one (lag = its sweep count) and the re-run checks the last one
+// (launch_jacobi_redo's last_*); see spec_lag_first.
 void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,
-                        int out_lo, int out_hi, hipStream_t s);
+                        int out_lo, int out_hi, hipStream_t s, int lag = 0);
 void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, int par,
                        hipStream_t s);
 // The whole tolerance-mode solve of a single-domain grid in one launch
@@ -258,7 +264,7 @@ bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *
 // buffer the host counts n launches ahead (k_spec_align; nyl * nx % 4 == 0)
 void launch_spec_align(const Geom &g, const Fields &f, int pass, int n, hipStream_t s);
 void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
-                        hipStream_t s);
+                        hipStream_t s, int last_it = 0, int last_par = 0, int last_T = 0);
 // dst[q] = max(dst[q], slots of q) for q < n, then zero those slots (before
 // an all-reduce of dst reads it).
 void launch_fold_slots(uint32_t *dst, uint32_t *slots, int n, hipStream_t s);

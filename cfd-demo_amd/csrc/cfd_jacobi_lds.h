@@ -716,11 +716,43 @@ __device__ __forceinline__ void spec_check_tail(const Geom &g, Ctl *ctl, uint32_
     ctl->spec_done = 0u;   // the next launch's tickets
 }
 
+// The lagged early-exit check (r5, single-domain speculative solves; replaces
+// the one-workgroup k_spec_check launch after every speculative launch): each
+// workgroup of the NEXT launch folds the T residual slot sets of launch lpar
+// itself (sweeps [it0, it0 + T), published a launch boundary earlier, never
+// reset during the solve -- the finalize folds and clears them) and finds the
+// first sweep below p_tol (model.rs:816).  Every workgroup computes the same
+// value; workgroup 0 publishes it (the launches that ran and, with `stop`, the
+// stop / re-run fields k_spec_check would set).  Returns that sweep's index,
+// T when none converged.  Called by every thread of the workgroup.
+__device__ __forceinline__ int spec_lag_first(const Geom &g, Ctl *ctl, const uint32_t *set0, int it0,
+                                              int T, int lpar, bool stop = true) {
+    __shared__ float e_s[kMaxTemporal];
+    const int wv = (int)threadIdx.x >> 6;
+    for (int s = wv; s < T; s += kLdsWaves) {
+        const float v = read_max(set0 + (size_t)s * kResSlots * kResStride, ctl->err[it0 + s]);
+        if ((threadIdx.x & 63) == 0) e_s[s] = v;
+    }
+    __syncthreads();
+    int j = 0;
+    while (j < T && !(e_s[j] < g.p_tol)) ++j;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->spec_launches = lpar + 1;
+        if (stop && j < T) {
+            ctl->spec_stop = 1;
+            ctl->spec_launch = lpar;
+            ctl->spec_redo = j + 1 < T ? j + 1 : 0;
+        }
+    }
+    return j;
+}
+
 template <int T, int FAST, int MODE>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
-    int wlo, int whi, int it, int spec_fold, int sums, float plim, float rlim, uint32_t *gslots) {
+    int wlo, int whi, int it, int spec_fold, int sums, float plim, float rlim, uint32_t *gslots,
+    int lag) {
     using M = LdsMarch<T, FAST, MODE>;
     [[maybe_unused]] constexpr bool RES = M::RES;   // the stamp guard's
     __shared__ f2 lds[kLdsWaves * M::D * 64];
@@ -748,12 +780,36 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
     } stamp_guard{st_rt0, st_t0, (unsigned long long)xcd_block(g)};
 #endif
     if (pass_off(ctl, pass)) return;
-    if (M::SPEC && ctl->spec_stop) return;   // an earlier launch of the solve converged
     int nst = 0;
-    if (M::REDO) {
-        nst = ctl->spec_redo;
+    if constexpr (M::SPEC) {
+        if (lag > 0) {
+            // the previous launch's check (k_spec_check's, a launch boundary
+            // after its residuals were published).  spec_stop is read once
+            // per workgroup: workgroup 0 of THIS launch may set it meanwhile,
+            // and the workgroup's waves must take one path (barriers below)
+            __shared__ int stop_s;
+            if (threadIdx.x == 0) stop_s = ctl->spec_stop;
+            __syncthreads();
+            if (stop_s) return;
+            if (spec_lag_first(g, ctl, res_slots - (size_t)lag * kResSlots * kResStride, it - lag, lag,
+                               par - 1) < lag)
+                return;   // it converged: this launch and every later one skip
+        } else if (ctl->spec_stop) {
+            return;   // an earlier launch of the solve converged
+        }
+    }
+    if constexpr (M::REDO) {
+        if (lag > 0 && !ctl->spec_stop) {
+            // the solve's last launch (par, sweeps [it, it + lag)) is checked
+            // here; only the count of launches that ran is published (the
+            // other workgroups read spec_stop / spec_redo / spec_launch)
+            const int j = spec_lag_first(g, ctl, res_slots, it, lag, par, false);
+            nst = j + 1 < lag ? j + 1 : 0;
+        } else {
+            nst = ctl->spec_redo;
+            par = ctl->spec_launch;   // re-run that launch: same source, same destination
+        }
         if (nst <= 0) return;
-        par = ctl->spec_launch;   // re-run that launch: same source, same destination
     }
     if constexpr (FAST == 1 && (MODE == 0 || MODE == 1)) {
         // the optimistic SUMS form (GRD 3, r5; sums: the grid allows the form
@@ -1174,7 +1230,7 @@ int lds_segments(const Geom &g, int nrows, int nwc, int pad, int occ_override = 
 
 template <int T, int MODE>
 void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
-                  uint32_t *rs, hipStream_t s) {
+                  uint32_t *rs, hipStream_t s, int lag = 0) {
     const int nch = g.nx / 2;
     const int nwc = cdiv(nch, LdsMarch<T, 1, MODE>::OUTL);
     const int nrows = out_hi - out_lo;
@@ -1213,7 +1269,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
     hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
                        rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, spec_fold, sums,  \
-                       plim, rlim, f.guard_slots)
+                       plim, rlim, f.guard_slots, lag)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);
     else if (g.fastdiv == 2)
@@ -1227,14 +1283,14 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
 // rs != nullptr), 2 (SPEC, rs = the first stage's slot set), 3 (REDO, T = 8).
 template <int T>
 void launch_lds_T(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
-                  uint32_t *rs, int mode, hipStream_t s) {
+                  uint32_t *rs, int mode, hipStream_t s, int lag = 0) {
     if (mode == 2) {
-        launch_lds_t<T, 2>(g, f, pass, par, it, out_lo, out_hi, rs, s);
+        launch_lds_t<T, 2>(g, f, pass, par, it, out_lo, out_hi, rs, s, lag);
         return;
     }
     if constexpr (T == 8) {
         if (mode == 3) {
-            launch_lds_t<8, 3>(g, f, pass, par, it, out_lo, out_hi, rs, s);
+            launch_lds_t<8, 3>(g, f, pass, par, it, out_lo, out_hi, rs, s, lag);
             return;
         }
     }
@@ -1345,9 +1401,9 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
 
 // per-translation-unit entry points (cfd_jacobi_lds*.hip)
 void launch_lds_t567(const Geom &g, const Fields &f, int T, int pass, int par, int it, int out_lo,
-                     int out_hi, uint32_t *rs, int mode, hipStream_t s);
+                     int out_hi, uint32_t *rs, int mode, hipStream_t s, int lag);
 void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
-                   uint32_t *rs, int mode, hipStream_t s);
+                   uint32_t *rs, int mode, hipStream_t s, int lag);
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,
                          int out_hi, uint32_t epoch, uint32_t *rs, hipStream_t s);
 

@@ -5,8 +5,8 @@
 namespace cfd {
 
 void launch_lds_t8(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
-                   uint32_t *rs, int mode, hipStream_t s) {
-    launch_lds_T<8>(g, f, pass, par, it, out_lo, out_hi, rs, mode, s);
+                   uint32_t *rs, int mode, hipStream_t s, int lag) {
+    launch_lds_T<8>(g, f, pass, par, it, out_lo, out_hi, rs, mode, s, lag);
 }
 
 bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int nblk, int out_lo,

@@ -1680,10 +1680,10 @@ bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, i
 }
 
 void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,
-                        int out_lo, int out_hi, hipStream_t s) {
+                        int out_lo, int out_hi, hipStream_t s, int lag) {
     if (out_hi <= out_lo) return;
     launch_lds(g, f, T, pass, it, par, out_lo, out_hi,
-               f.err_slots + (size_t)it * kResSlots * kResStride, s, 2);
+               f.err_slots + (size_t)it * kResSlots * kResStride, s, 2, lag);
 }
 
 void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, int par,
@@ -1692,9 +1692,11 @@ void launch_spec_check(const Geom &g, const Fields &f, int pass, int it, int T, 
 }
 
 void launch_jacobi_redo(const Geom &g, const Fields &f, int pass, int out_lo, int out_hi,
-                        hipStream_t s) {
+                        hipStream_t s, int last_it, int last_par, int last_T) {
     if (out_hi <= out_lo) return;
-    launch_lds(g, f, kMaxTemporal, pass, 0, 0, out_lo, out_hi, nullptr, s, 3);
+    launch_lds(g, f, kMaxTemporal, pass, last_it, last_par, out_lo, out_hi,
+               last_T > 0 ? f.err_slots + (size_t)last_it * kResSlots * kResStride : nullptr, s, 3,
+               last_T);
 }
 
 void launch_spec_align(const Geom &g, const Fields &f, int pass, int n, hipStream_t s) {

@@ -1154,17 +1154,25 @@ struct cfd_model {
                 // launch runs kSpecT sweeps with every sweep's residual, a check
                 // finds the reference's early exit (model.rs:816), and the
                 // converged launch is re-run with exactly its sweeps
+                // the check: by default (r5) each launch checks the previous
+                // one and the re-run checks the last (spec_lag_first);
+                // CFD_SPEC_LAG=0 launches k_spec_check after every launch,
+                // CFD_SPEC_FOLD=1 has the launch's last workgroup check it
+                const bool lag = spec_lag_env && !spec_fold_env;
+                int prev_T = 0, last_it = 0;
                 for (int it = 0; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
-                    launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream);
-                    // the launch's last workgroup checks (spec_check_tail) unless
-                    // CFD_SPEC_FOLD=1; by default a one-workgroup launch after it
-                    if (!spec_fold_env) launch_spec_check(g, f, pass, it, T, launches, stream);
+                    launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream, lag ? prev_T : 0);
+                    if (!spec_fold_env && !lag) launch_spec_check(g, f, pass, it, T, launches, stream);
+                    prev_T = T;
+                    last_it = it;
                     it += T;
                     ++launches;
                 }
-                if (iters > 0) launch_jacobi_redo(g, f, pass, lo_g, hi_g, stream);
+                if (iters > 0)
+                    launch_jacobi_redo(g, f, pass, lo_g, hi_g, stream, last_it, launches - 1,
+                                       lag ? prev_T : 0);
             } else if (tmax <= 1) {
                 for (int it = 0; it < iters; ++it)
                     launch_jacobi_sweep(g, f, pass, it, lo_g, hi_g,
@@ -1538,6 +1546,11 @@ struct cfd_model {
     bool spec_fold_env = [] {
         const char *e = getenv("CFD_SPEC_FOLD");
         return e && atoi(e) != 0;
+    }();
+    // the lagged early-exit check (r5, spec_lag_first): CFD_SPEC_LAG=0 opts out
+    bool spec_lag_env = [] {
+        const char *e = getenv("CFD_SPEC_LAG");
+        return !(e && atoi(e) == 0);
     }();
     bool spec_mode() const {
         return spec_env && !sharded() && g.tol_enabled &&
