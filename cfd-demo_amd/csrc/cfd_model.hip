@@ -1154,9 +1154,9 @@ struct cfd_model {
                 // launch runs kSpecT sweeps with every sweep's residual, a check
                 // finds the reference's early exit (model.rs:816), and the
                 // converged launch is re-run with exactly its sweeps
-                // the check: by default (r5) each launch checks the previous
-                // one and the re-run checks the last (spec_lag_first);
-                // CFD_SPEC_LAG=0 launches k_spec_check after every launch,
+                // the check: a one-workgroup k_spec_check launch after every
+                // launch; CFD_SPEC_LAG=1 (r5) has each launch check the
+                // previous one and the re-run check the last (spec_lag_first);
                 // CFD_SPEC_FOLD=1 has the launch's last workgroup check it
                 const bool lag = spec_lag_env && !spec_fold_env;
                 int prev_T = 0, last_it = 0;
@@ -1451,11 +1451,12 @@ struct cfd_model {
     // blocks (enqueue_solve): per block one T-row p' exchange, one speculative
     // launch publishing every sweep's residual, one all-reduce of the block's
     // T residuals and the device-side check -- instead of a launch, a fold,
-    // an all-reduce, an exchange and a host read per sweep.  CFD_SPEC_SLABS=0
-    // keeps the host-driven per-sweep loop.
+    // an all-reduce, an exchange and a host read per sweep.  Opt-in
+    // (CFD_SPEC_SLABS=1) until it has run on the hardware
+    // (tests/test_gpu_optin_r5.py); by default the host-driven per-sweep loop.
     bool spec_slab_env = [] {
         const char *e = getenv("CFD_SPEC_SLABS");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     bool spec_slab_ok() const {
         return sharded() && spec_env && spec_slab_env && params.pressure_solver == CFD_SOLVER_JACOBI &&
@@ -1547,10 +1548,11 @@ struct cfd_model {
         const char *e = getenv("CFD_SPEC_FOLD");
         return e && atoi(e) != 0;
     }();
-    // the lagged early-exit check (r5, spec_lag_first): CFD_SPEC_LAG=0 opts out
+    // the lagged early-exit check (r5, spec_lag_first): opt-in (CFD_SPEC_LAG=1)
+    // until it has run on the hardware (tests/test_gpu_optin_r5.py)
     bool spec_lag_env = [] {
         const char *e = getenv("CFD_SPEC_LAG");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     bool spec_mode() const {
         return spec_env && !sharded() && g.tol_enabled &&

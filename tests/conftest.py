@@ -12,6 +12,8 @@ for p in (ROOT, os.path.join(ROOT, "cfd-demo_amd"), os.path.join(ROOT, "oracle")
 # bench.py self-launch).  They run after every single-process parity file, so
 # a harness fault there cannot hide the oracle checks behind it under -x (r4).
 MULTI_PROCESS_FILES = ("test_gpu_rccl.py",)
+# r5's opt-in paths not yet run on the hardware: after everything else
+LAST_FILES = ("test_gpu_optin_r5.py",)
 
 
 def pytest_configure(config):
@@ -20,7 +22,7 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(session, config, items):
-    late = [it for it in items if os.path.basename(str(it.fspath)) in MULTI_PROCESS_FILES]
-    if late:
-        early = [it for it in items if os.path.basename(str(it.fspath)) not in MULTI_PROCESS_FILES]
-        items[:] = early + late
+    def rank(it):
+        name = os.path.basename(str(it.fspath))
+        return 2 if name in LAST_FILES else 1 if name in MULTI_PROCESS_FILES else 0
+    items[:] = sorted(items, key=rank)   # stable: file order kept within each group

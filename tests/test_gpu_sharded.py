@@ -415,31 +415,3 @@ def test_sharded_multigrid_partitioned_levels(monkeypatch, n, nx, ny, tol, part)
     check_against_oracle(st, grid, dict(bc_kind=1, viscosity=1.0 / 400.0, pressure_solver=2,
                                         corrector_passes=2, tol_enabled=int(tol)), 3,
                          FIELDS + ("rhs",))
-
-
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("n,p_tol,depth", [(2, 1e-4, 8), (4, 1e-3, 8), (3, 3e-5, 6), (2, 2e-4, 4)])
-def test_sharded_spec_tolerance_mode(monkeypatch, n, p_tol, depth):
-    """r5: the reference's tolerance mode on slabs as speculative T-sweep
-    blocks (one T-row p' exchange, one speculative launch, one all-reduce of
-    the block's residuals and a device-side check per block; the converged
-    block re-run and aligned to the host-counted buffer) equals the oracle --
-    early exits at every p_tol, 20 corrector passes -- and the host-driven
-    per-sweep loop it replaces (CFD_SPEC_SLABS=0), with a fraction of its
-    collective calls."""
-    import cfdamd
-    grid = cfdamd.cavity_grid(128, 128)
-    params = cfdamd.SimulationParams.cavity(100.0, 50, p_tol=p_tol)
-    calls = {}
-    states = {}
-    for env in ("1", "0"):
-        monkeypatch.setenv("CFD_SPEC_SLABS", env)
-        st, ex = run_sharded(n, grid, params, 3, depth, extra=lambda m: m.comm_calls)
-        states[env] = st
-        calls[env] = ex[0]
-    check_against_oracle(states["1"], grid, dict(bc_kind=1, viscosity=0.01, p_tol=p_tol), 3,
-                         FIELDS + ("rhs",))
-    a, b = assemble(states["1"], grid.nx), assemble(states["0"], grid.nx)
-    for f in FIELDS:
-        assert_bitwise(f"spec vs host-driven:{f}", a[f], b[f])
-    assert calls["1"] * 3 < calls["0"], calls

@@ -48,16 +48,13 @@ def _compare(tag, m, o):
     return int(s.jacobi_sweeps_total)
 
 
-@pytest.fixture(params=["resident", "launches", "check_launches"])
+@pytest.fixture(params=["resident", "launches"])
 def solve_form(request, monkeypatch):
-    """Every parity case runs three times: as the small-grid default, the
-    whole solve in one resident launch (k_jacobi_resident); as the per-launch
-    speculative path (CFD_RESIDENT=0: k_jacobi_lds MODE 2 launches, each
-    checking the previous one's early exit, r5's lagged check, and the redo
-    checking the last); and with a k_spec_check launch after every launch
-    (CFD_SPEC_LAG=0, r4's form)."""
+    """Every parity case runs twice: as the small-grid default, the whole
+    solve in one resident launch (k_jacobi_resident), and as the per-launch
+    speculative path (CFD_RESIDENT=0: k_jacobi_lds MODE 2 + checks + redo).
+    The r5 lagged check runs the same cases in test_gpu_optin_r5.py."""
     monkeypatch.setenv("CFD_RESIDENT", "1" if request.param == "resident" else "0")
-    monkeypatch.setenv("CFD_SPEC_LAG", "0" if request.param == "check_launches" else "1")
     return request.param
 
 
@@ -212,40 +209,6 @@ def test_spec_fold_matches_check_launch(monkeypatch, p_tol):
     for f in STATE:
         assert_bitwise(f"spec fold on/off:{f}", states[1][f], states[0][f])
     assert states[0]["jacobi_sweeps_total"] == states[1]["jacobi_sweeps_total"]
-
-
-def test_spec_lag_matches_check_launch_at_every_exit(monkeypatch):
-    """The lagged check (each speculative launch decides whether the previous
-    one converged; the re-run decides for the last) against k_spec_check
-    launches (CFD_SPEC_LAG=0) on a sweep of tolerances that puts the early exit
-    at every position of an 8-sweep launch, the first and last launch
-    included: identical bits, sweep counts and residuals."""
-    import cfdamd
-    monkeypatch.setenv("CFD_RESIDENT", "0")
-    grid = cfdamd.cavity_grid(192, 160)
-    seen = set()
-    for p_tol in (3e-3, 1e-3, 5e-4, 2e-4, 1e-4, 5e-5):
-        params = cfdamd.SimulationParams.cavity(200.0, 50, p_tol=p_tol)
-        out = []
-        for env in ("0", "1"):
-            monkeypatch.setenv("CFD_SPEC_LAG", env)
-            m = cfdamd.Model(grid, params, device=0)
-            sw = []
-            prev = 0
-            for _ in range(12):
-                m.update()
-                tot = m.get_residuals().jacobi_sweeps_total
-                sw.append(tot - prev)
-                prev = tot
-            out.append((m.get_state(), sw))
-            m.close()
-        for f in STATE + ("last_p_residual",):
-            assert_bitwise(f"lag vs check tol {p_tol}:{f}", out[1][0][f], out[0][0][f])
-        assert out[0][1] == out[1][1], (p_tol, out[0][1], out[1][1])
-        seen.update(out[1][1])
-    # early exits were taken (per-step totals over the corrector passes'
-    # solves that are not whole 50-sweep solves), at several positions
-    assert len({s % 8 for s in seen}) >= 4 and any(s % 50 for s in seen), sorted(seen)
 
 
 def test_resident_deadline_fault_is_loud_and_recoverable(monkeypatch):
