@@ -7,7 +7,10 @@ rows cfd_plan_sweep names (a numpy emulation of k_jacobi's arithmetic and
 fused p' boundary stores), exchanges exactly the rows cfd_plan_halo names via
 torch.distributed send/recv, and the gathered result must equal the
 single-domain oracle (oracle/cfd_oracle.c) word for word.  The exchange
-geometry of u and v is checked by shipping global row ids.
+geometry of u and v is checked by shipping global row ids.  Since r5 the
+tolerance mode's speculative slab blocks (enqueue_spec_slabs) run the same
+way: exits at every block position equal the oracle's p', residual and sweep
+count, with one exchange and one all-reduce per block.
 """
 import ctypes as C
 import os
@@ -324,3 +327,182 @@ def test_single_domain_blocks_split_evenly():
             assert it == iters
             assert len(Ts) == -(-iters // t_max), (t_max, iters, Ts)
             assert max(Ts) - min(Ts) <= 1 and Ts == sorted(Ts, reverse=True), (t_max, iters, Ts)
+
+
+# ---------------------------------------------------------------------------
+# r5: the tolerance mode on slabs as speculative T-sweep blocks
+# (enqueue_spec_slabs, cfd_model.hip; opt-in CFD_SPEC_SLABS=1).  The same
+# schedule in numpy over gloo: per block ONE p' exchange T rows deep, T sweeps
+# of the owned rows (sweep s recomputing T-1-s ghost rows each side), ONE
+# all-reduce of the block's T residuals, the first sweep below p_tol ends the
+# solve (later blocks skip); the converged block re-runs with exactly its
+# sweeps from its untouched source, the result is copied to the buffer the
+# host counted (one flip per block), and one 1-row exchange follows.
+
+def simd_end(nx):
+    e = 1
+    while e + 8 <= nx - 1:
+        e += 8
+    return e
+
+
+def spec_block(src, rhs, g0, lo, hi, T, nx, ny, j0, dx, dy):
+    """T sweeps from src over owned rows [lo, hi) (cones into the ghosts);
+    returns the last sweep's buffer and every sweep's residual over the owned
+    rows (columns [1, simd_end), model.rs:755-772)."""
+    cur, nxt = src.copy(), src.copy()
+    se = simd_end(nx)
+    errs = []
+    for s_ in range(T):
+        e = T - 1 - s_
+        a, b = max(lo - e, 1 - j0), min(hi + e, ny - 1 - j0)
+        sweep_rows(cur, nxt, rhs, g0, a, b, nx, ny, j0, dx, dy)
+        d = np.abs(nxt[lo + g0:hi + g0, 1:se] - cur[lo + g0:hi + g0, 1:se])
+        errs.append(F(d.max()) if d.size else F(0))
+        cur, nxt = nxt, cur
+    return cur, errs
+
+
+def _spec_worker(rank, n, port, cases, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    try:
+        out = []
+        for (nx, ny, hg, iters, seed, p_tol) in cases:
+            P, RHS = _spec_inputs(nx, ny, seed)
+            dx, dy = F(F(2.0) / F(nx)), F(F(1.0) / F(ny))
+            j0, j1 = plan_slab(ny, n, rank)
+            nyl = j1 - j0
+            g0 = hg
+            lo, hi = max(0, 1 - j0), min(nyl, ny - 1 - j0)
+            bufs = [np.zeros((nyl + 2 * hg, nx), F) for _ in range(2)]
+            rhs = np.zeros((nyl + 2 * hg, nx), F)
+            bufs[0][g0:g0 + nyl] = P[j0:j1]
+            rhs[g0:g0 + nyl] = RHS[j0:j1]
+            exchange(bufs[0], g0, plan_halo(2, nyl, hg, rank, n), rank, n)
+            exchange(rhs, g0, plan_halo(2, nyl, hg, rank, n), rank, n)
+            Tm = min(8, hg)
+            nb = -(-iters // Tm)
+            it, launches, stop, collectives = 0, 0, None, 1   # the rhs exchange
+            for b in range(nb):
+                T = iters // nb + (1 if b < iters % nb else 0)
+                src = bufs[launches & 1]
+                exchange(src, g0, plan_halo(2, nyl, T, rank, n), rank, n)
+                collectives += 2
+                if stop is None:   # the device skips the blocks after the exit
+                    res, errs = spec_block(src, rhs, g0, lo, hi, T, nx, ny, j0, dx, dy)
+                    e = torch.tensor(np.array(errs, F))
+                    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+                    errs = e.numpy()
+                    # owned rows and the fused global boundary rows
+                    dst = bufs[(launches + 1) & 1]
+                    dst[g0:g0 + nyl] = res[g0:g0 + nyl]
+                    hit = [k for k in range(T) if errs[k] < F(p_tol)]
+                    if hit:
+                        stop = (launches, hit[0] + 1, F(errs[hit[0]]), it + hit[0] + 1)
+                    last = (F(errs[-1]), it + T)
+                it += T
+                launches += 1
+            if stop is not None:
+                L, nsw, resid, sweeps = stop
+                src = bufs[L & 1]
+                res, _ = spec_block(src, rhs, g0, lo, hi, nsw, nx, ny, j0, dx, dy)
+                bufs[(L + 1) & 1][g0:g0 + nyl] = res[g0:g0 + nyl]
+                if (launches - (L + 1)) & 1:   # k_spec_align
+                    bufs[launches & 1][g0:g0 + nyl] = bufs[(L + 1) & 1][g0:g0 + nyl]
+            else:
+                resid, sweeps = last
+            final = bufs[launches & 1]
+            exchange(final, g0, plan_halo(2, nyl, 1, rank, n), rank, n)
+            collectives += 1
+            # the ghost row the corrector reads holds the neighbour's owned row
+            if rank > 0:
+                a_, _ = plan_slab(ny, n, rank - 1)
+                prev = torch.empty(nx, dtype=torch.float32)
+                dist.recv(prev, rank - 1)
+                assert np.array_equal(final[g0 - 1], prev.numpy())
+            if rank < n - 1:
+                dist.send(torch.from_numpy(np.ascontiguousarray(final[g0 + nyl - 1])), rank + 1)
+            mine = torch.from_numpy(np.ascontiguousarray(final[g0:g0 + nyl]))
+            if rank == 0:
+                parts = [mine.numpy()]
+                for r in range(1, n):
+                    a, b_ = plan_slab(ny, n, r)
+                    t = torch.empty((b_ - a, nx), dtype=torch.float32)
+                    dist.recv(t, r)
+                    parts.append(t.numpy())
+                out.append((np.concatenate(parts).ravel(), float(resid), int(sweeps), collectives))
+            else:
+                dist.send(mine, 0)
+        if rank == 0:
+            results.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _spec_inputs(nx, ny, seed):
+    """A smooth-ish start whose Jacobi residual decays through the tolerances
+    below within 50 sweeps (random noise of amplitude 1e-3, zero rhs)."""
+    rng = np.random.default_rng(seed)
+    P = (1e-3 * rng.uniform(-1, 1, (ny, nx))).astype(F)
+    RHS = np.zeros((ny, nx), F)
+    return P, RHS
+
+
+def _oracle_solve(nx, ny, iters, seed, p_tol):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleModel
+    P, RHS = _spec_inputs(nx, ny, seed)
+    o = OracleModel(nx, ny, 2.0, 1.0, jacobi_iters=iters, tol_enabled=1, p_tol=p_tol)
+    o.field("p_prime")[:] = P.ravel()
+    o.field("rhs")[:] = RHS.ravel()
+    s0 = o.scalars().jacobi_sweeps_total
+    r = o.jacobi()
+    return o.field("p_prime").copy(), F(r), int(o.scalars().jacobi_sweeps_total - s0)
+
+
+def _spec_cases():
+    """Tolerances just above the single-domain residual after k sweeps, so the
+    solve ends at or before sweep k: exits in the first block, mid-block, at
+    a block's last sweep, and none (k = 50)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleModel
+    cases = []
+    for (nx, ny, hg, seed) in ((32, 48, 8, 21), (24, 40, 5, 22), (16, 44, 3, 23)):
+        P, RHS = _spec_inputs(nx, ny, seed)
+        for k in (1, 3, 8, 13, 22, 50):
+            o = OracleModel(nx, ny, 2.0, 1.0, jacobi_iters=k, tol_enabled=0)
+            o.field("p_prime")[:] = P.ravel()
+            o.field("rhs")[:] = RHS.ravel()
+            r = F(o.jacobi())
+            cases.append((nx, ny, hg, 50, seed, float(np.nextafter(r, F(1)))))
+    return cases
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_sharded_spec_blocks_match_single_domain(n):
+    cases = _spec_cases()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spec_worker, args=(r, n, port, cases, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    exits = set()
+    for (nx, ny, hg, iters, seed, p_tol), (res, resid, sweeps, coll) in zip(cases, got):
+        want, wres, wsweeps = _oracle_solve(nx, ny, iters, seed, p_tol)
+        assert np.array_equal(res.view(np.uint32), want.view(np.uint32)), (nx, ny, hg, p_tol)
+        assert F(resid).view(np.uint32) == wres.view(np.uint32) and sweeps == wsweeps, \
+            (nx, ny, hg, p_tol, resid, wres, sweeps, wsweeps)
+        exits.add(sweeps)
+        # one exchange + one all-reduce per block, plus the rhs and final
+        # exchanges: against 2 calls per sweep for the host-driven loop
+        assert coll == 2 * -(-iters // min(8, hg)) + 2 < 2 * iters
+    assert len(exits) >= 4 and 50 in exits, sorted(exits)
