@@ -458,15 +458,6 @@ class Model:
         return int(n.value)
 
     @property
-    def chain_stats(self) -> dict:
-        """The chained 8-sweep march (k_jacobi_chain): launches run and row
-        groups re-run in the reference's form after the optimistic SUMS
-        form's guard failed (cfd_get_chain_stats; life of the model)."""
-        a, b = C.c_uint64(), C.c_uint64()
-        check("cfd_get_chain_stats", load().cfd_get_chain_stats(self._hh(), C.byref(a), C.byref(b)))
-        return dict(launches=int(a.value), fallbacks=int(b.value))
-
-    @property
     def comm_calls(self) -> int:
         """Halo-exchange groups + all-reduces enqueued (cfd_get_comm_calls)."""
         n = C.c_uint64()

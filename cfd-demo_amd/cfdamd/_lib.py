@@ -20,7 +20,7 @@ EXPORTS = [
     "cfd_get_residuals", "cfd_get_state", "cfd_set_state", "cfd_get_masks", "cfd_synchronize",
     "cfd_profile_sweeps", "cfd_timing_begin", "cfd_timing_end", "cfd_timing_phases",
     "cfd_timing_phase_ms", "cfd_timing_exchange_ms", "cfd_get_halo_depth",
-    "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_get_persist_blocks", "cfd_get_persist_steals", "cfd_get_persist_sums", "cfd_get_chain_stats", "cfd_get_recoveries", "cfd_get_comm_calls", "cfd_get_resident_solves", "cfd_get_jacobi_geometry", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block", "cfd_plan_overlap", "cfd_plan_chain",
+    "cfd_get_kernel_config", "cfd_get_jacobi_kernel", "cfd_get_persist_blocks", "cfd_get_persist_steals", "cfd_get_persist_sums", "cfd_get_recoveries", "cfd_get_comm_calls", "cfd_get_resident_solves", "cfd_get_jacobi_geometry", "cfd_plan_slab", "cfd_plan_sweep", "cfd_plan_halo", "cfd_plan_block", "cfd_plan_overlap",
     "cfd_render", "cfd_derive_field", "cfd_last_error", "cfd_abi_version", "cfd_destroy",
     "cfd_get_config", "cfd_run_start", "cfd_run_stop", "cfd_run_pause", "cfd_run_resume",
     "cfd_run_set_params", "cfd_run_request_snapshot", "cfd_run_last_snapshot",
@@ -140,7 +140,6 @@ def load():
         "cfd_get_persist_blocks": (i32, [vp, C.POINTER(i32)]),
         "cfd_get_persist_steals": (i32, [vp, C.POINTER(C.c_uint64)]),
         "cfd_get_persist_sums": (i32, [vp, C.POINTER(C.c_uint64)]),
-        "cfd_get_chain_stats": (i32, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "cfd_get_recoveries": (i32, [vp, C.POINTER(C.c_uint64)]),
         "cfd_get_comm_calls": (i32, [vp, C.POINTER(C.c_uint64)]),
         "cfd_get_resident_solves": (i32, [vp, C.POINTER(C.c_uint64)]),
@@ -152,7 +151,6 @@ def load():
                                  C.POINTER(i32)]),
         "cfd_plan_halo": (i32, [i32, i32, i32, i32, i32, C.POINTER(i32)]),
         "cfd_plan_overlap": (i32, [i32, i32, i32, i32, i32, i32, C.POINTER(i32)]),
-        "cfd_plan_chain": (i32, [i32, i32, i32, i32, i32, i32] + [C.POINTER(i32)] * 5),
         "cfd_plan_block": (i32, [i32, i32, i32, i32, i32, i32, i32, C.POINTER(i32),
                                  C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "cfd_render": (i32, [vp, i32, C.POINTER(C.c_uint8), FP]),

@@ -147,7 +147,9 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
             int n = iters;
             if (g.tol_enabled && iters > 0) {
                 n = 1;
-                while (n < iters && __uint_as_float(c->err[n - 1]) >= g.p_tol) ++n;
+                // model.rs:816: only `max_error < tolerance` exits (a NaN
+                // residual runs on, as every sweep kernel's check does)
+                while (n < iters && !(__uint_as_float(c->err[n - 1]) < g.p_tol)) ++n;
             }
             const float res = n > 0 ? __uint_as_float(c->err[n - 1]) : 0.0f;
             // one buffer flip per launch: per sweep with the tolerance on,
@@ -169,10 +171,6 @@ __device__ __forceinline__ void solve_finalize_body(const Geom &g, const Fields 
     __syncthreads();
     if (go_s)
         for (int k = threadIdx.x; k < iters; k += blockDim.x) c->err[k] = 0u;
-    // the next solve's SUMS guard chain starts from empty sets
-    if (f.guard_slots)
-        for (int q = threadIdx.x; q < kGuardSets * kResSlots; q += blockDim.x)
-            f.guard_slots[(size_t)(q / kResSlots) * kResSlots * kResStride + (q % kResSlots) * kResStride] = 0u;
 }
 
 // One reference Jacobi update (model.rs:775-793) of the 4 consecutive

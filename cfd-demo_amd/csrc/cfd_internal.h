@@ -52,10 +52,8 @@ constexpr int kPersistBlockBits = 10;
 static_assert((1 << kPersistBlockBits) > kMaxSweeps / 8, "persistent flag layout");
 constexpr int kPersistMaxGroups = 16384;   // tiles (wave columns x row groups)
 constexpr size_t kPersistWords = (size_t)(kPersistMaxGroups + kPersistHeadLines) * kPersistFlagStride;
-// slot sets: kMaxSweeps per-sweep residual sets, then red (4), vis (2), 2
-// spare, the SUMS guard of the per-launch solve (kGuardSets, from +8), 3 spare;
-// then the persistent solve's words
-constexpr int kGuardSets = 5;
+// slot sets: kMaxSweeps per-sweep residual sets, then red (4), vis (2), 10
+// spare; then the persistent solve's words
 constexpr size_t kSlotWords = (size_t)(kMaxSweeps + 16) * kResSlots * kResStride + kPersistWords;
 
 // Device-resident control block: every data-dependent decision of
@@ -86,8 +84,7 @@ struct Ctl {
     // (0: none, it converged on its last stage); spec_launches: launches run
     // (the finalize's buffer flips).  All 0 between solves.
     int32_t spec_stop, spec_redo, spec_launch, spec_launches;
-    uint32_t spec_done;     // tickets of the running speculative launch (spec_check_tail); 0 between
-                            // launches
+    uint32_t spec_done;     // (unused since r6; keeps the layout)
     int32_t go[kMaxPasses + 1];      // go[p]: pass p of the corrector loop runs
     uint32_t err[kMaxSweeps];        // per-sweep max |p'new - p'| as f32 bits
 };
@@ -150,11 +147,6 @@ struct Fields {
     // the RCCL watchdog's evidence of forward progress
     uint32_t *host_progress;
     uint32_t *persist;   // kPersistWords words after the slot sets (see kPersistFlagStride)
-    // kGuardSets spread sets (zeroed by every solve's finalize; r4's
-    // whole-solve SUMS guard used them), then the diagnostics words of set
-    // kGuardSets: [0] per-launch blocks run in the optimistic SUMS form, [1]
-    // chain launches, [2] waves / row groups re-run in the reference's form
-    uint32_t *guard_slots;
 };
 
 // ---- launchers (cfd_kernels.hip) ----
@@ -228,19 +220,6 @@ bool launch_lds_persist8(const Geom &g, const Fields &f, int pass, int par0, int
 // the solve's last launch's, checked by the re-run (see k_jacobi_lds)
 void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par, int out_lo,
                 int out_hi, uint32_t *res_slots, hipStream_t s, int mode = 0, int lag = 0);
-// r5: an 8-sweep block of a single-domain solve as the chained march
-// (cfd_jacobi_chain.hip: a workgroup's four wave segments hand their boundary
-// rows to each other instead of recomputing cones); false: its plan does not
-// fit (nothing launched).  chain_enabled(): CFD_JACOBI_CHAIN=1 (opt-in).
-bool launch_lds_chain8(const Geom &g, const Fields &f, int pass, int par, int out_lo, int out_hi,
-                       uint32_t *rs, hipStream_t s);
-bool chain_enabled();
-// the chain runs the 8-sweep blocks over rows [out_lo, out_hi) of this grid
-bool chain_applies(const Geom &g, int out_lo, int out_hi);
-// its plan: wave columns, row groups per column, the chain groups' D (d0; the
-// first nhi groups d0 + 1) and the first (edge) group's rows
-bool chain_plan(const Geom &g, int out_lo, int out_hi, int occ, int *nwc, int *ngrp, int *d0, int *nhi,
-                int *elo);
 // Speculative temporal blocking for the tolerance mode (model.rs:748-819):
 // the launch starting at sweep `it` runs T sweeps (kind 5) and publishes
 // every sweep's residual; k_spec_check folds them, finds the first sweep
@@ -381,6 +360,9 @@ void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s);
 // Slabs with persistent runs (r5): copy this rank's abort word (persist[1],
 // a persistent solve timed out) into Ctl::red[6] before the step all-reduce
 void launch_abort_to_red(const Fields &f, hipStream_t s);
+// ... and, after its all-reduce outside a step, back into this rank's abort
+// flag and host word (as the step finalize does)
+void launch_abort_from_red(const Fields &f, hipStream_t s);
 
 // Jacobi kernel geometry (exported for the roofline bookkeeping in bench).
 constexpr int kJacRowsPerWave = 16;

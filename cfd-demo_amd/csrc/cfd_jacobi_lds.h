@@ -117,13 +117,10 @@ constexpr int ring_depth(int T, int PD, int G) {
 // overflow included; a subnormal h + v is exact).  k_jacobi_persist proves
 // that bound per task before it picks SUMS (its guard); otherwise, and for
 // every other launch, the reference's form runs.
-// GRD 3 (r5, the default per-launch form; it replaces r4's whole-solve guard
-// chain, GRD 1/2, which measured no faster than the reference's form): OPTIMISTIC SUMS -- the wave runs the
-// SUMS form while tracking max |p'| of every input row it loads (stage 1's
-// Tp, plus B and C at stage 1's first slot) and max |rhs|, then checks the
-// bound (lds_block); where it fails the wave re-runs its march in the
-// reference's form.
-template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
+// (r5's optimistic per-wave SUMS form for per-launch solves and r4's
+// whole-solve guard lost their A/B against the reference's form and were
+// removed in r6: every per-launch march runs the reference's form.)
+template <int T, int FAST, int MODE, bool SUMS = false>
 struct LdsMarch {
     static constexpr bool RES = MODE == 1 || MODE == 5, SPEC = MODE == 2, REDO = MODE == 3;
     // MODE 4 (PERSIST): a block of k_jacobi_persist; p' moves between
@@ -138,7 +135,7 @@ struct LdsMarch {
 #ifndef CFD_PROBE_NOTRACK
 #define CFD_PROBE_NOTRACK 0   // (diagnostic builds: no guard tracking)
 #endif
-    static constexpr bool TRACK_IN = (PERSIST && !SUMS && !CFD_PROBE_NOTRACK) || GRD == 3;
+    static constexpr bool TRACK_IN = PERSIST && !SUMS && !CFD_PROBE_NOTRACK;
     static constexpr bool TRACK_OUT = PERSIST && !CFD_PROBE_NOTRACK;
     static_assert(!SUMS || FAST == 1, "SUMS: reciprocal multiply");
     static constexpr int PLD_AUX = PERSIST ? 16 : CFD_LDS_LD_AUX;
@@ -191,34 +188,6 @@ struct LdsMarch {
     int nyl_;
 
     LdsMarch() = default;
-    // the same march state in the other form (the chain guard's SUMS twin,
-    // lds_block): member by member, so the state stays in registers
-    template <bool S2, int G2>
-    __device__ __forceinline__ explicit LdsMarch(const LdsMarch<T, FAST, MODE, S2, G2> &o) {
-#pragma unroll
-        for (int a = 0; a < T; ++a)
-#pragma unroll
-            for (int b = 0; b < NW; ++b) W[a][b] = o.W[a][b];
-#pragma unroll
-        for (int q = 0; q < PD; ++q) {
-            PQ[q] = o.PQ[q];
-            RQ[q] = o.RQ[q];
-        }
-        ring = o.ring;
-        lane = o.lane;
-        k_first = o.k_first, S = o.S, lo_clamp = o.lo_clamp, hi_clamp = o.hi_clamp, nch = o.nch;
-        g_first = o.g_first, g_last = o.g_last, g_top = o.g_top, g_zero = o.g_zero;
-        row_bytes = o.row_bytes, wbase = o.wbase;
-        ch = o.ch, vo_ld = o.vo_ld, vo_st = o.vo_st, abase = o.abase, dir = o.dir;
-        e0 = o.e0, e1 = o.e1;
-        dx_sq = o.dx_sq, r_dx_sq = o.r_dx_sq, dy_sq = o.dy_sq, r_dy_sq = o.r_dy_sq;
-        denom = o.denom, r_denom = o.r_denom;
-        rs_p = o.rs_p, rs_r = o.rs_r, rs_d = o.rs_d;
-        m = o.m, omax = o.omax, imax = o.imax, rmax = o.rmax;
-#pragma unroll
-        for (int q = 0; q < (SPEC ? T : 1); ++q) mm[q] = o.mm[q];
-        r0v = o.r0v, r1v = o.r1v, nst = o.nst, nyl_ = o.nyl_;
-    }
 
     __device__ __forceinline__ int act(int vrow) const { return abase + dir * vrow; }
 
@@ -321,11 +290,6 @@ struct LdsMarch {
                 if (s == 1) {
                     imax = fmaxf(fmaxf(imax, fabsf(Tp.x)), fabsf(Tp.y));
                     rmax = fmaxf(fmaxf(rmax, fabsf(rh.x)), fabsf(rh.y));
-                    // GRD 3: the wave's own bound also covers the first two
-                    // input rows (B and C of stage 1's first slot)
-                    if (GRD == 3 && GUARD == 0 && V_ == start(1))
-                        imax = fmaxf(fmaxf(imax, fmaxf(fabsf(B.x), fabsf(B.y))),
-                                     fmaxf(fabsf(C.x), fabsf(C.y)));
                 }
             }
             f2 n = stage<E>(B, C, Tp, rh);
@@ -472,30 +436,13 @@ struct LdsMarch {
 // trk (persistent blocks): per wave, trk[3 w .. 3 w + 2] = max |p'| of the
 // rows it stored, of the p' rows it loaded and of the rhs rows it used (the
 // last two only in the reference's form; 0 where not tracked or no rows).
-// GRD 3 (the optimistic SUMS form, r5): a wave's T sweeps stay bitwise in
-// the form when every p' input it loads is below plim / 2 = 2^123 / R, every
-// rhs value below rlim = 2^124 and the drift T 0.1875 max|rhs| / R (a sweep
-// moves max |p'| by at most that: |pu| <= M + |rhs| / (4R), p_new = 0.75 pu
-// + 0.25 p) below plim / 2: then every h R, v R the sweeps form is < 2^126,
-// the form's exactness bound (see LdsMarch).  NaN: max ignores it and it
-// propagates as the same operand in either form; +-Inf fails the bound.
-__device__ __forceinline__ bool sums_bound(float im, float rm, float plim, float rlim, int T,
-                                           const Geom &g) {
-    const float drift = 0.1875f * (float)T * rm * g.dx_sq;   // dx^2 == 1 / R exactly (FAST 1)
-    return im < 0.5f * plim && rm < rlim && drift < 0.5f * plim;
-}
-
-template <int T, int FAST, int MODE, bool SUMS = false, int GRD = 0>
+template <int T, int FAST, int MODE, bool SUMS = false>
 __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           float *__restrict__ pb, const float *__restrict__ rhs,
                                           Ctl *ctl, uint32_t *res_slots, int par, int out_lo,
                                           int out_hi, int nwc, int nseg, int wlo, int whi, f2 *lds,
-                                          int nst, int bid, int spec_fold = 0,
-                                          float *trk = nullptr, uint32_t *gset = nullptr,
-                                          uint32_t *grhs = nullptr, const uint32_t *gprev = nullptr,
-                                          float plim = 0.0f, float rlim = 0.0f, int r0o = -1,
-                                          int r1o = -1) {
-    using M = LdsMarch<T, FAST, MODE, SUMS, GRD>;
+                                          int nst, int bid, float *trk = nullptr) {
+    using M = LdsMarch<T, FAST, MODE, SUMS>;
     constexpr bool RES = M::RES;
     M w;
     w.nst = nst;
@@ -510,9 +457,8 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     // first / last one (lighter where that segment runs the boundary-row path)
     const long total = nseg == 1 ? 16 : wlo + whi + 16L * (nseg - 2);
     auto cum = [&](int i) -> long { return i <= 0 ? 0 : (i >= nseg ? total : wlo + 16L * (i - 1)); };
-    // r0o >= 0: the caller's rows for this wave (k_jacobi_chain's edge groups)
-    const int r0 = r0o >= 0 ? r0o : out_lo + (int)(cum(seg) * nrows / total);
-    const int r1 = r0o >= 0 ? r1o : out_lo + (int)(cum(seg + 1) * nrows / total);
+    const int r0 = out_lo + (int)(cum(seg) * nrows / total);
+    const int r1 = out_lo + (int)(cum(seg + 1) * nrows / total);
     if (r0 >= r1) return;
     const int nx = g.nx;
     w.ring = lds + wave * M::D * 64;
@@ -596,25 +542,16 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         w.RQ[q] = w.ld(w.rs_r, w.k_first + q);
     }
     // the march and what the launch publishes
-    bool redo = false;   // GRD 3: the bound failed, the reference's form re-runs the wave
-    auto finish = [&](auto &wx) {
-    using MX = typename std::remove_reference<decltype(wx)>::type;
     if (row_edge)
-        wx.template run<MX::kCol | MX::kRow>();
+        w.template run<M::kCol | M::kRow>();
     else if (col_edge)
-        wx.template run<MX::kCol>();
+        w.template run<M::kCol>();
     else
-        wx.template run<0>();
-    if constexpr (GRD == 3) {
-        if (!sums_bound(wave_max(wx.imax), wave_max(wx.rmax), plim, rlim, T, g)) {
-            redo = true;   // nothing published: the re-run does
-            return;
-        }
-    }
+        w.template run<0>();
     if (M::PERSIST && trk) {
-        const float o = wave_max(out_lane ? wx.omax : 0.0f);
-        const float im = M::TRACK_IN ? wave_max(wx.imax) : 0.0f;
-        const float rm = M::TRACK_IN ? wave_max(wx.rmax) : 0.0f;
+        const float o = wave_max(out_lane ? w.omax : 0.0f);
+        const float im = M::TRACK_IN ? wave_max(w.imax) : 0.0f;
+        const float rm = M::TRACK_IN ? wave_max(w.rmax) : 0.0f;
         if (lane == 0) {
             trk[3 * wave] = o;
             trk[3 * wave + 1] = im;
@@ -622,38 +559,18 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
         }
     }
     if (M::SPEC) {
-        // spec_fold: returning atomics, all of the wave's in flight at once,
-        // then one wait (the launch's last workgroup reads them: spec_check_tail)
-        unsigned acc = 0u;
 #pragma unroll
         for (int s = 0; s < T; ++s) {
-            const float ms = wave_max(out_lane ? wx.mm[s] : 0.0f);
-            if (lane == 0 && ms > 0.0f) {
-                uint32_t *slot = res_slots + (size_t)s * kResSlots * kResStride +
-                                 ((bid * kLdsWaves + wave) & (kResSlots - 1)) * kResStride;
-                if (spec_fold)
-                    acc |= __hip_atomic_fetch_max(slot, __float_as_uint(ms), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                else
-                    atomicMax(slot, __float_as_uint(ms));
-            }
+            const float ms = wave_max(out_lane ? w.mm[s] : 0.0f);
+            if (lane == 0 && ms > 0.0f)
+                atomicMax(res_slots + (size_t)s * kResSlots * kResStride +
+                              ((bid * kLdsWaves + wave) & (kResSlots - 1)) * kResStride,
+                          __float_as_uint(ms));
         }
-        if (spec_fold) asm volatile("s_waitcnt vmcnt(0)" ::"v"(acc) : "memory");
     }
     if (!RES) return;
-    const float m = wave_max(out_lane ? wx.m : 0.0f);
+    const float m = wave_max(out_lane ? w.m : 0.0f);
     if (lane == 0) publish_max(res_slots, bid * kLdsWaves + wave, m);
-    };
-    finish(w);
-    if constexpr (GRD == 3) {
-        if (redo) {
-            // gset: the fallback counter (cfd_get_chain_stats)
-            if (lane == 0 && gset) atomicAdd(gset, 1u);
-            lds_block<T, FAST, MODE, false, 0>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc,
-                                               nseg, wlo, whi, lds, nst, bid, spec_fold, trk, nullptr,
-                                               nullptr, nullptr, plim, rlim, r0o, r1o);
-        }
-    }
 }
 
 // Minimum waves per SIMD the register allocation must allow (the SPEC
@@ -665,57 +582,6 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
 constexpr int lds_min_waves(int mode) {
     return mode == 2 ? CFD_LDS_SPEC_WPE : (CFD_LDS_WPE > 0 ? CFD_LDS_WPE : 1);
 }
-// The speculative launch's own early-exit check (r4, replaces k_spec_check's
-// launch; opt-in with CFD_SPEC_FOLD=1 -- on MI355X the device-scope ticket and
-// the returning atomics cost more than the one-workgroup launch they save:
-// C3 parity mode 11.28 vs 10.83 ms/step, profiles/r4/ab_parity_r4g.log):
-// every workgroup publishes its sweeps'
-// residual maxima with RETURNING atomics and waits for them, then takes a
-// ticket (a returning device-scope add); the workgroup that draws the last
-// ticket sees every residual of the launch and folds them (atomic exchange
-// with 0: read and reset at the memory side, where the atomics were
-// performed), finds the first of the launch's sweeps below p_tol
-// (model.rs:816) and sets spec_stop / spec_launch / spec_redo for the launches
-// that follow (a kernel boundary away).  k_spec_check's logic and bits.
-inline bool spec_fold_on() {
-    const char *e = getenv("CFD_SPEC_FOLD");
-    return e && atoi(e) != 0;
-}
-template <int T>
-__device__ __forceinline__ void spec_check_tail(const Geom &g, Ctl *ctl, uint32_t *res_slots, int it,
-                                                int par) {
-    __shared__ int last_s;
-    __syncthreads();   // every wave's residual atomics have returned
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(&ctl->spec_done, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        last_s = t == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last_s) return;
-    const int wv = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
-    for (int s = wv; s < T; s += kLdsWaves) {
-        uint32_t *set = res_slots + (size_t)s * kResSlots * kResStride;
-        const unsigned v = lane < kResSlots ? __hip_atomic_exchange(set + lane * kResStride, 0u,
-                                                                     __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                            : 0u;
-        const float m = fmaxf(wave_max(__uint_as_float(v)), __uint_as_float(ctl->err[it + s]));
-        if (lane == 0) ctl->err[it + s] = __float_as_uint(m);
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    int j = 0;
-    while (j < T && !(__uint_as_float(ctl->err[it + j]) < g.p_tol)) ++j;
-    ctl->spec_launches = par + 1;
-    if (j < T) {
-        ctl->spec_stop = 1;
-        ctl->spec_launch = par;
-        ctl->spec_redo = j + 1 < T ? j + 1 : 0;
-    }
-    ctl->spec_done = 0u;   // the next launch's tickets
-}
-
 // The lagged early-exit check (r5, single-domain speculative solves; replaces
 // the one-workgroup k_spec_check launch after every speculative launch): each
 // workgroup of the NEXT launch folds the T residual slot sets of launch lpar
@@ -751,8 +617,7 @@ template <int T, int FAST, int MODE>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
-    int wlo, int whi, int it, int spec_fold, int sums, float plim, float rlim, uint32_t *gslots,
-    int lag) {
+    int wlo, int whi, int it, int lag) {
     using M = LdsMarch<T, FAST, MODE>;
     [[maybe_unused]] constexpr bool RES = M::RES;   // the stamp guard's
     __shared__ f2 lds[kLdsWaves * M::D * 64];
@@ -811,23 +676,8 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         }
         if (nst <= 0) return;
     }
-    if constexpr (FAST == 1 && (MODE == 0 || MODE == 1)) {
-        // the optimistic SUMS form (GRD 3, r5; sums: the grid allows the form
-        // at all, see LdsMarch): every wave checks its own bound after its
-        // march and re-runs in the reference's form where it fails
-        if (sums) {
-            constexpr size_t kSet = (size_t)kResSlots * kResStride;
-            uint32_t *const cnt = gslots ? gslots + kGuardSets * kSet : nullptr;   // [0] launches, [2] re-runs
-            if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) atomicAdd(cnt, 1u);
-            lds_block<T, FAST, MODE, true, 3>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc,
-                                              nseg, wlo, whi, lds, nst, xcd_block(g), spec_fold, nullptr,
-                                              cnt ? cnt + 2 : nullptr, nullptr, nullptr, plim, rlim);
-            return;
-        }
-    }
     lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc, nseg, wlo,
-                             whi, lds, nst, xcd_block(g), spec_fold);
-    if (M::SPEC && spec_fold) spec_check_tail<T>(g, ctl, res_slots, it, par);
+                             whi, lds, nst, xcd_block(g));
 }
 
 // Persistent fixed-count solve: ONE launch runs nblk blocks of T sweeps
@@ -1105,19 +955,19 @@ __global__ __launch_bounds__(kLdsWaves * 64, CFD_PERSIST_WPE) void k_jacobi_pers
             if (fast) {
                 if (res)
                     lds_block<T, FAST, 5, true>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi,
-                                                nwc, nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+                                                nwc, nseg, wlo, whi, lds, 0, tile, trk_s);
                 else
                     lds_block<T, FAST, 4, true>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi,
-                                                nwc, nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+                                                nwc, nseg, wlo, whi, lds, 0, tile, trk_s);
             }
         }
         if (!fast) {
             if (res)
                 lds_block<T, FAST, 5>(g, pa, pb, rhs, ctl, res_slots, par0 + b, out_lo, out_hi, nwc,
-                                      nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+                                      nseg, wlo, whi, lds, 0, tile, trk_s);
             else
                 lds_block<T, FAST, 4>(g, pa, pb, rhs, ctl, nullptr, par0 + b, out_lo, out_hi, nwc,
-                                      nseg, wlo, whi, lds, 0, tile, 0, trk_s);
+                                      nseg, wlo, whi, lds, 0, tile, trk_s);
         }
         // every wave's max |p'| stored, with (before) the flag: the next
         // block's guard of the neighbours (written through, drained below)
@@ -1247,29 +1097,9 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int reach = T + 2;
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
-    const int spec_fold = MODE == 2 && spec_fold_on() ? 1 : 0;
-    // the optimistic SUMS form (GRD 3): reciprocal multiply, dx^2 == dy^2
-    // with a power-of-two reciprocal R >= 1 (h R, v R exact below overflow),
-    // fixed-count launches.  Opt-in (CFD_JACOBI_SUMS=1): with its input
-    // tracking it measured slower than the reference's form, 5.03 vs 4.97 us
-    // per sweep at 4096^2 (profiles/r5/prof_r5f/ab_sums.log).  Read per launch
-    // (tests switch it).
-    int sums = 0;
-    float plim = 0.0f, rlim = 0.0f;
-    if ((MODE == 0 || MODE == 1) && g.fastdiv == 1 && g.dx_sq == g.dy_sq && g.r_dx_sq == g.r_dy_sq) {
-        const char *ue = getenv("CFD_JACOBI_SUMS");
-        int e2 = 0;
-        const float R = g.r_dx_sq;
-        if (ue && atoi(ue) == 1 && R >= 1.0f && std::frexp(R, &e2) == 0.5f) {
-            sums = 1;
-            plim = std::ldexp(1.0f, 124) / R;
-            rlim = std::ldexp(1.0f, 124);
-        }
-    }
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
     hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
-                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, spec_fold, sums,  \
-                       plim, rlim, f.guard_slots, lag)
+                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, lag)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);
     else if (g.fastdiv == 2)

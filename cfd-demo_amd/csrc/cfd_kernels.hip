@@ -1230,6 +1230,16 @@ __global__ void k_abort_to_red(Fields f) {
         f.ctl->red[6] = __hip_atomic_load(f.persist + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
 }
 
+// The all-reduced abort word back into this rank's abort flag and host word
+// (k_step_finalize's part of it, for the entry points with no step finalize:
+// cfd_piso_step, cfd_pressure_solve).
+__global__ void k_abort_from_red(Fields f) {
+    if (threadIdx.x != 0 || !ld_ctl_t<false>(&f.ctl->red[6])) return;
+    if (f.persist) __hip_atomic_store(f.persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f.host_nonfinite)
+        __hip_atomic_store(f.host_nonfinite + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void k_step_finalize(Geom g, Fields f) { step_finalize_body<false>(g, f); }
 
 // One row of k_correct_finish4's work for the 4 columns i0..i0+3 of local
@@ -1653,23 +1663,10 @@ void launch_jacobi_block(const Geom &g, const Fields &f, int pass, int it, int p
         launch_pipe4(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
     else if (g.tb_kind == 4)
         launch_pipe2(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
-    else if (g.tb_kind == 5) {
-        // r5: the chained march (cfd_jacobi_chain.hip) where its plan fits
-        if (T == 8 && chain_enabled() && launch_lds_chain8(g, f, pass, par, out_lo, out_hi, rs, s))
-            return;
+    else if (g.tb_kind == 5)
         launch_lds(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
-    } else
+    else
         launch_tb1(g, f, T, pass, it, par, out_lo, out_hi, rs, s);
-}
-
-// CFD_JACOBI_CHAIN=1: 8-sweep blocks of single-domain solves as the chained
-// march (opt-in: r5 measured it slower than the per-launch march, 5.48 vs
-// 4.95 us per sweep at 4096^2, profiles/r5/ -- its opening and closing slots
-// are as long as full ones, see cfd_jacobi_chain.hip).  Read per call so
-// tests can switch it.
-bool chain_enabled() {
-    const char *e = getenv("CFD_JACOBI_CHAIN");
-    return e && atoi(e) != 0;
 }
 
 bool launch_jacobi_persist(const Geom &g, const Fields &f, int pass, int par0, int nblk,
@@ -1845,6 +1842,10 @@ void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s) {
 
 void launch_abort_to_red(const Fields &f, hipStream_t s) {
     hipLaunchKernelGGL(k_abort_to_red, dim3(1), dim3(64), 0, s, f);
+}
+
+void launch_abort_from_red(const Fields &f, hipStream_t s) {
+    hipLaunchKernelGGL(k_abort_from_red, dim3(1), dim3(64), 0, s, f);
 }
 
 void launch_step_finalize(const Geom &g, const Fields &f, hipStream_t s) {

@@ -303,6 +303,27 @@ struct cfd_model {
         return exchange(buf ? FLD_PP1 : FLD_PP0, HALO_PP, rows, st);
     }
 
+    // rhs ghosts `rhs_rows` deep and p' buffer `buf`'s `pp_rows` deep in ONE
+    // RCCL group (one collective call: the speculative slab solve's first block)
+    int exchange_rhs_pp(int rhs_rows, int buf, int pp_rows) {
+        if (!sharded()) return 0;
+        ++comm_calls;
+        const int pid = buf ? FLD_PP1 : FLD_PP0;
+        if (hub) {
+            int rc = exchange_local(FLD_RHS, HALO_PP, rhs_rows, stream);
+            if (rc) return rc;
+            return exchange_local(pid, HALO_PP, pp_rows, stream);
+        }
+        if (!comm) return fail(CFD_ERCCL, "the RCCL communicator was aborted after an earlier failure");
+        phase_mark(2, false, stream);
+        RCCL_TRY(ncclGroupStart());
+        int rc = exchange_ops(FLD_RHS, HALO_PP, rhs_rows, stream);
+        if (!rc) rc = exchange_ops(pid, HALO_PP, pp_rows, stream);
+        RCCL_OP(ncclGroupEnd());
+        phase_mark(2, true, stream);
+        return rc;
+    }
+
     int allreduce_max_u32(uint32_t *dev, size_t n) {
         if (!sharded()) return 0;
         ++comm_calls;
@@ -1156,15 +1177,14 @@ struct cfd_model {
                 // converged launch is re-run with exactly its sweeps
                 // the check: a one-workgroup k_spec_check launch after every
                 // launch; CFD_SPEC_LAG=1 (r5) has each launch check the
-                // previous one and the re-run check the last (spec_lag_first);
-                // CFD_SPEC_FOLD=1 has the launch's last workgroup check it
-                const bool lag = spec_lag_env && !spec_fold_env;
+                // previous one and the re-run check the last (spec_lag_first)
+                const bool lag = spec_lag_env;
                 int prev_T = 0, last_it = 0;
                 for (int it = 0; it < iters;) {
                     int T, lo, hi, exch;
                     plan_block((int)j0, g.nyl, g.ny, 0, it, kMaxTemporal, iters, &T, &lo, &hi, &exch);
                     launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream, lag ? prev_T : 0);
-                    if (!spec_fold_env && !lag) launch_spec_check(g, f, pass, it, T, launches, stream);
+                    if (!lag) launch_spec_check(g, f, pass, it, T, launches, stream);
                     prev_T = T;
                     last_it = it;
                     it += T;
@@ -1459,21 +1479,53 @@ struct cfd_model {
         return e && atoi(e) != 0;
     }();
     bool spec_slab_ok() const {
+        // (k_spec_align moves float4s from pp + hg * nx: 16-B aligned rows)
         return sharded() && spec_env && spec_slab_env && params.pressure_solver == CFD_SOLVER_JACOBI &&
-               g.hg >= 2 && g.nyl >= 2 * kMaxTemporal && ((size_t)g.nyl * g.nx) % 4 == 0;
+               g.hg >= 2 && g.nyl >= 2 * kMaxTemporal && ((size_t)g.nyl * g.nx) % 4 == 0 &&
+               ((size_t)g.hg * g.nx) % 4 == 0;
     }
+    // r6: the host's view of the speculative blocks.  After its all-reduce a
+    // block's T residuals -- the same values on every rank -- are copied to
+    // pinned host words; the host reads block 0 at once (from rest a solve
+    // usually ends in its first sweeps) and every later block one block
+    // behind, and enqueues no block (and, in enqueue_piso, no corrector pass)
+    // past the one where the solve has ended.  Every rank reads the same
+    // values, so every rank stops at the same block and the collective
+    // sequences stay matched; the device's own check (k_spec_check, the
+    // go flags) stays authoritative for the bits.  So a solve's collectives
+    // track its convergence (r5 enqueued all blocks of all 20 passes:
+    // 1,014 calls against the host-driven loop's 30, GPUTEST_r05).
+    static constexpr int kSpecRing = 4;
+    uint32_t *h_spec = nullptr;               // kSpecRing x kMaxTemporal pinned words
+    hipEvent_t ev_spec[kSpecRing] = {};
+    bool spec_converged = false;              // the last speculative slab solve ended early
     int enqueue_spec_slabs(int pass, hipEvent_t e1) {
         const int iters = params.jacobi_iters;
         const int Tm = std::min(kMaxTemporal, g.hg);
         const int lo = std::max(0, 1 - (int)j0), hi = std::min(g.nyl, (int)g.ny - 1 - (int)j0);
-        // every block reads rhs rows T deep into the ghosts
-        int rc = exchange(FLD_RHS, HALO_PP, g.hg);
-        if (rc) return rc;
         const int nb = iters > 0 ? (iters + Tm - 1) / Tm : 0;
-        int it = 0, launches = 0;
-        for (int b = 0; b < nb; ++b) {
+        int it = 0, launches = 0, checked = 0, rc = 0;
+        int blk_T[kSpecRing] = {};
+        bool stop = false;
+        // reads block `checked`'s all-reduced residuals (waits for them)
+        auto check_next = [&]() -> int {
+            const int slot = checked % kSpecRing;
+            int rc2 = wait_done(ev_spec[slot]);
+            if (rc2) return rc2;
+            for (int k = 0; k < blk_T[slot] && !stop; ++k) {
+                float e;
+                std::memcpy(&e, (const void *)&h_spec[slot * kMaxTemporal + k], 4);
+                stop = e < params.p_tol;   // model.rs:816 (NaN: no exit)
+            }
+            ++checked;
+            return 0;
+        };
+        for (int b = 0; b < nb && !stop; ++b) {
             const int T = iters / nb + (b < iters % nb ? 1 : 0);   // even split, no short tail
-            rc = exchange_pp((host_cur + launches) & 1, T);         // the block's source, T rows deep
+            // the block's source, T rows deep; every block reads rhs rows T
+            // deep into the ghosts: the first block's exchange carries them
+            rc = b == 0 ? exchange_rhs_pp(g.hg, (host_cur + launches) & 1, T)
+                        : exchange_pp((host_cur + launches) & 1, T);
             if (rc) return rc;
             launch_jacobi_spec(g, f, pass, it, launches, T, lo, hi, stream);
             launch_fold_slots(f.ctl->err + it, f.err_slots + (size_t)it * kResSlots * kResStride, T,
@@ -1481,9 +1533,26 @@ struct cfd_model {
             rc = allreduce_max_u32(f.ctl->err + it, (size_t)T);   // every rank decides alike
             if (rc) return rc;
             launch_spec_check(g, f, pass, it, T, launches, stream);
+            const int slot = b % kSpecRing;
+            HIP_TRY(hipMemcpyAsync(&h_spec[slot * kMaxTemporal], f.ctl->err + it, 4 * (size_t)T,
+                                   hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipEventRecord(ev_spec[slot], stream));
+            blk_T[slot] = T;
             it += T;
             ++launches;
+            while (!stop && checked <= (b == 0 ? 0 : b - 1)) {
+                rc = check_next();
+                if (rc) return rc;
+            }
         }
+        // the pass loop's break (pass >= 1 with a pass after it) needs the
+        // solve's outcome: the last blocks too
+        const bool need = pass >= 1 && pass < params.corrector_passes;
+        while (need && !stop && checked < launches) {
+            rc = check_next();
+            if (rc) return rc;
+        }
+        spec_converged = stop;
         if (iters > 0) {
             launch_jacobi_redo(g, f, pass, lo, hi, stream);
             launch_spec_align(g, f, pass, launches, stream);
@@ -1543,10 +1612,6 @@ struct cfd_model {
     bool spec_env = [] {
         const char *e = getenv("CFD_SPEC");
         return !(e && atoi(e) == 0);
-    }();
-    bool spec_fold_env = [] {
-        const char *e = getenv("CFD_SPEC_FOLD");
-        return e && atoi(e) != 0;
     }();
     // the lagged early-exit check (r5, spec_lag_first): opt-in (CFD_SPEC_LAG=1)
     // until it has run on the hardware (tests/test_gpu_optin_r5.py)
@@ -1662,11 +1727,15 @@ struct cfd_model {
                     launch_corrector(g, f, pass, dt_override, stream);
             };
             corrector(0);
+            const bool spec_slabs = sharded() && g.tol_enabled && spec_slab_ok();
             for (int pass = 1; pass <= passes; ++pass) {
                 if (!fuse) pass_head(pass, dt_override);
                 rc = enqueue_solve(pass);
                 if (rc) return rc;
                 corrector(pass);
+                // slabs: the host knows where the loop ends (enqueue_spec_slabs)
+                // and enqueues no pass the device would skip (model.rs:721-723)
+                if (spec_slabs && spec_converged) break;
             }
         } else {
             first_divergence(-1);
@@ -1804,6 +1873,21 @@ struct cfd_model {
             int rc = enqueue_update(k == n - 1);
             if (rc) return rc;
         }
+        return 0;
+    }
+
+    // Slabs with persistent runs, entry points outside Model::update
+    // (cfd_piso_step, cfd_pressure_solve): a rank whose persistent solve timed
+    // out tells every rank through an all-reduce of the abort word, so every
+    // rank recovers at its next synchronisation and replays the same calls
+    // (inside a step the step all-reduce carries it, enqueue_update)
+    int abort_allreduce() {
+        if (!(sharded() && persist_env && persist_sharded_env)) return 0;
+        launch_abort_to_red(f, stream);
+        int rc = allreduce_max_u32(f.ctl->red + 6, 1);
+        if (rc) return rc;
+        launch_abort_from_red(f, stream);
+        HIP_TRY(hipGetLastError());
         return 0;
     }
 
@@ -1964,6 +2048,9 @@ struct cfd_model {
         for (hipEvent_t e : ev_res)
             if (e) (void)hipEventDestroy(e);
         if (h_res) (void)hipHostFree(h_res);
+        for (hipEvent_t e : ev_spec)
+            if (e) (void)hipEventDestroy(e);
+        if (h_spec) (void)hipHostFree(h_spec);
         for (void *ptr : {(void *)u_all, (void *)v_all, (void *)uo_all, (void *)vo_all,
                           (void *)us_all, (void *)vs_all, (void *)p, (void *)rhs,
                           (void *)pp_all[0], (void *)pp_all[1], (void *)mask_u, (void *)mask_v,
@@ -2243,6 +2330,8 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     *(volatile uint32_t *)(m->h_nonfinite + 2) = 0u;
     HIP_TRY(hipHostMalloc((void **)&m->h_res, 4 * cfd_model::kResRing, hipHostMallocDefault));
     for (hipEvent_t &e : m->ev_res) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void **)&m->h_spec, 4 * cfd_model::kSpecRing * kMaxTemporal, hipHostMallocDefault));
+    for (hipEvent_t &e : m->ev_spec) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char *to = getenv("CFD_RCCL_TIMEOUT_S")) m->rccl_timeout_s = std::max(1.0, atof(to));
 
     // obstacle masks and cell list from cell centres (model.rs:235-260)
@@ -2332,7 +2421,6 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     f.err_slots = m->slots;
     f.red_slots = m->slots + (size_t)kMaxSweeps * kResSlots * kResStride;
     f.vis_slots = f.red_slots + (size_t)4 * kResSlots * kResStride;
-    f.guard_slots = m->slots + (size_t)(kMaxSweeps + 8) * kResSlots * kResStride;
     f.persist = m->slots + (size_t)(kMaxSweeps + 16) * kResSlots * kResStride;
 
     Ctl c0;
@@ -2620,13 +2708,13 @@ int cfd_piso_step(cfd_model *m, float dt_sub) {
     if (!m) return fail(CFD_EINVAL, "null model");
     HIP_TRY(hipSetDevice(m->device));
     if (int rc = m->ck_begin()) return rc;
-    m->ck_record([m, dt_sub]() {
+    auto run = [m, dt_sub]() {
         int rc = m->exchange_uv();
-        return rc ? rc : m->enqueue_piso(dt_sub);
-    });
-    int rc = m->exchange_uv();
-    if (rc) return rc;
-    return m->enqueue_piso(dt_sub);
+        if (!rc) rc = m->enqueue_piso(dt_sub);
+        return rc ? rc : m->abort_allreduce();
+    };
+    m->ck_record(run);
+    return run();
 }
 
 int cfd_pressure_solve(cfd_model *m, float *residual_out) {
@@ -2637,8 +2725,12 @@ int cfd_pressure_solve(cfd_model *m, float *residual_out) {
         return m->enqueue_solve_host_driven(residual_out);
     }
     if ((rc = m->ck_begin())) return rc;
-    m->ck_record([m]() { return m->enqueue_solve(-1); });
-    rc = m->enqueue_solve(-1);
+    auto run = [m]() {
+        int rc2 = m->enqueue_solve(-1);
+        return rc2 ? rc2 : m->abort_allreduce();
+    };
+    m->ck_record(run);
+    rc = run();
     if (rc) return rc;
     Ctl c;
     rc = m->read_ctl(&c);
@@ -2973,7 +3065,6 @@ int cfd_get_kernel_config(const cfd_model *m, int *fastdiv, int *temporal) {
 
 int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name_len) {
     if (!m) return fail(CFD_EINVAL, "null model");
-    (void)hipSetDevice(m->device);   // chain_applies asks the occupancy API
     const bool spec = m->spec_mode();
     const bool resident = m->resident_mode();
     const int T = spec ? kMaxTemporal : m->g.tol_enabled ? 1 : m->t_max;
@@ -2989,9 +3080,6 @@ int cfd_get_jacobi_kernel(const cfd_model *m, int *kind, char *name, size_t name
             snprintf(buf, sizeof buf, "k_jacobi<%d, %d>", kJacRowsPerWave, m->g.fastdiv);
         else if (k == 1)
             snprintf(buf, sizeof buf, "k_jacobi_tb<%d, %d>", T, m->g.fastdiv);
-        else if (k == 5 && T == 8 && !m->sharded() &&
-                 chain_applies(m->g, 1 - (int)m->j0, (int)m->g.ny - 1 - (int)m->j0))
-            snprintf(buf, sizeof buf, "k_jacobi_chain<%d, %d, 0>", T, m->g.fastdiv);
         else if (k == 5)
             snprintf(buf, sizeof buf, "k_jacobi_lds<%d, %d, 0>", T, m->g.fastdiv);
         else
@@ -3034,23 +3122,9 @@ int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks) {
     if (!m || !blocks) return fail(CFD_EINVAL, "null argument");
     int rc = m->sync();
     if (rc) return rc;
-    uint32_t v = 0, w = 0;
+    uint32_t v = 0;
     HIP_TRY(hipMemcpy(&v, m->f.persist + 3, 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&w, m->f.guard_slots + (size_t)kGuardSets * kResSlots * kResStride, 4,
-                      hipMemcpyDeviceToHost));
-    *blocks = (uint64_t)v + w;   // persistent blocks + per-launch blocks in the SUMS form
-    return 0;
-}
-
-int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks) {
-    if (!m) return fail(CFD_EINVAL, "null model");
-    int rc = m->sync();
-    if (rc) return rc;
-    uint32_t w[3] = {0, 0, 0};
-    HIP_TRY(hipMemcpy(w, m->f.guard_slots + (size_t)kGuardSets * kResSlots * kResStride, 12,
-                      hipMemcpyDeviceToHost));
-    if (launches) *launches = w[1];
-    if (fallbacks) *fallbacks = w[2];
+    *blocks = v;   // persistent blocks run in the SUMS form
     return 0;
 }
 
@@ -3104,15 +3178,6 @@ int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, i
 int cfd_plan_overlap(int nyl, int halo_depth, int rank, int n_ranks, int lo, int hi, int *out6) {
     if (!out6 || n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(CFD_EINVAL, "bad plan_overlap arguments");
     return plan_overlap(nyl, halo_depth, rank, n_ranks, lo, hi, out6);
-}
-
-int cfd_plan_chain(int nx, int ny, int n_cu, int occ, int out_lo, int out_hi, int *nwc, int *ngrp,
-                   int *d0, int *nhi, int *elo) {
-    if (nx < 2 || ny < 2 || n_cu < 1 || occ < 1 || !nwc || !ngrp || !d0 || !nhi || !elo)
-        return fail(CFD_EINVAL, "bad plan_chain arguments");
-    Geom g{};
-    g.nx = nx, g.ny = ny, g.j0 = 0, g.nyl = ny, g.n_cu = n_cu;
-    return chain_plan(g, out_lo, out_hi, occ, nwc, ngrp, d0, nhi, elo) ? 1 : 0;
 }
 
 int cfd_plan_halo(int kind, int nyl, int depth, int rank, int n_ranks, int *out6) {

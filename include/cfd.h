@@ -264,20 +264,9 @@ int cfd_get_persist_steals(cfd_model *m, uint64_t *steals);
 /* 8-sweep blocks run in the SUMS form -- (h + v) / dx^2 for h / dx^2 +
  * v / dy^2, one instruction per column pair and sweep fewer, taken only where
  * a guard proves it bitwise: persistent-solve blocks per tile
- * (k_jacobi_persist's per-task guard) plus per-launch blocks (k_jacobi_lds,
- * r5: the optimistic form -- every wave checks its own bound after its march
- * and re-runs in the reference's form where it fails, cfd_get_chain_stats
- * counts those) -- summed over the model's life.  Synchronises.  (new;
- * diagnostics) */
+ * (k_jacobi_persist's per-task guard), summed over the model's life.
+ * Synchronises.  (new; diagnostics) */
 int cfd_get_persist_sums(cfd_model *m, uint64_t *blocks);
-/* The chained 8-sweep march (k_jacobi_chain, r5: a workgroup's four wave
- * segments hand their boundary rows to each other instead of recomputing
- * warm-up cones; opt-in CFD_JACOBI_CHAIN=1 for single-domain fixed-count
- * solves where its plan fits): chain launches run, and the chain row groups
- * or per-launch waves (k_jacobi_lds) whose optimistic SUMS form failed its
- * bound and were re-run in the reference's form, summed over the model's
- * life.  Synchronises.  (new; diagnostics) */
-int cfd_get_chain_stats(cfd_model *m, uint64_t *launches, uint64_t *fallbacks);
 /* Collective calls this (sharded) model has enqueued: halo-exchange groups
  * and all-reduces, summed over its life (0 unsharded).  (new; diagnostics) */
 int cfd_get_comm_calls(const cfd_model *m, uint64_t *n);
@@ -317,15 +306,6 @@ int cfd_plan_overlap(int nyl, int halo_depth, int rank, int n_ranks, int lo, int
  * [out_lo, out_hi); halo_depth <= 0 means unsharded. */
 int cfd_plan_block(int j0, int nyl, int ny, int halo_depth, int it, int t_max, int iters, int *T,
                    int *out_lo, int *out_hi, int *exchange);
-
-/* The chained 8-sweep march's plan for a single-domain nx x ny grid, rows
- * [out_lo, out_hi), n_cu CUs, occ workgroups per CU (k_jacobi_chain): wave
- * columns, row groups per column, the chain groups' D (d0; the first nhi of
- * them d0 + 1: 4D + 2 - 16 rows each) and the first edge group's rows (the
- * last edge group takes the rest).  Returns 1 when a chain fits, 0 when the
- * per-launch march runs instead. */
-int cfd_plan_chain(int nx, int ny, int n_cu, int occ, int out_lo, int out_hi, int *nwc, int *ngrp,
-                   int *d0, int *nhi, int *elo);
 
 /* Visualisation modes of App (src/app.rs:505-509 VisualizationMode). */
 typedef enum { CFD_VIS_PRESSURE = 0, CFD_VIS_VELOCITY = 1, CFD_VIS_VORTICITY = 2 } cfd_vis_mode;

@@ -12,6 +12,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from _util import assert_bitwise
@@ -88,8 +89,10 @@ def test_sharded_spec_tolerance_mode(monkeypatch, n, p_tol, depth):
     the block's residuals and a device-side check per block; the converged
     block re-run and aligned to the host-counted buffer) equals the oracle --
     early exits at every p_tol, 20 corrector passes -- and the host-driven
-    per-sweep loop it replaces (CFD_SPEC_SLABS=0), with a fraction of its
-    collective calls."""
+    per-sweep loop it replaces (CFD_SPEC_SLABS=0).  From rest every solve
+    ends in its first sweeps: r6's host-side stop makes no more collective
+    calls than the host-driven loop there (r5 enqueued every block of every
+    pass: 1,014 calls against 30)."""
     import cfdamd
     grid = cfdamd.cavity_grid(128, 128)
     params = cfdamd.SimulationParams.cavity(100.0, 50, p_tol=p_tol)
@@ -105,7 +108,69 @@ def test_sharded_spec_tolerance_mode(monkeypatch, n, p_tol, depth):
     a, b = assemble(states["1"], grid.nx), assemble(states["0"], grid.nx)
     for f in FIELDS:
         assert_bitwise(f"spec vs host-driven:{f}", a[f], b[f])
-    assert calls["1"] * 3 < calls["0"], calls
+    assert calls["1"] <= calls["0"], calls
+
+
+@pytest.mark.timeout(300)
+def test_sharded_spec_long_solves_fewer_collectives(monkeypatch):
+    """A developed cavity injected into 2 slabs (set_state) with a tolerance
+    no sweep reaches (p_tol 1e-9): every solve runs its 50 sweeps and the
+    pass loop all 20 passes, the regime the speculative blocks are for.  The
+    blocks (7 exchanges + 7 all-reduces + 1 ghost row per solve) make at most
+    a third of the host-driven loop's collective calls (2 per sweep), and
+    both equal the single-domain model bit for bit."""
+    import cfdamd
+    from test_gpu_sharded import _slab_slices
+    import threading
+    grid = cfdamd.cavity_grid(128, 128)
+    base = cfdamd.SimulationParams.cavity(100.0, 50)
+    m = cfdamd.Model(grid, base, device=0)
+    m.update_n(30)
+    st0 = m.get_state()
+    m.close()
+    params = cfdamd.SimulationParams.cavity(100.0, 50, p_tol=1e-9)
+    ref = cfdamd.Model(grid, params, device=0)
+    ref.set_state(**st0)
+    ref.update_n(2)
+    want = ref.get_state()
+    ref.close()
+    calls = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("CFD_SPEC_SLABS", env)
+        hub = cfdamd.LocalHub(2)
+        out, models, errors = [None] * 2, [None] * 2, []
+
+        def worker(r):
+            try:
+                mm = cfdamd.Model(grid, params, device=0, n_ranks=2, rank=r, local_hub=hub)
+                models[r] = mm
+                mm.set_state(**_slab_slices(st0, grid.nx, mm.j0, mm.j1))
+                c0 = mm.comm_calls
+                mm.update_n(2)
+                mm.synchronize()
+                out[r] = (mm.j0, mm.j1, mm.get_state(), mm.comm_calls - c0)
+            except Exception as e:   # surfaced below
+                errors.append(e)
+
+        ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(240)
+        for mm in models:
+            if mm is not None:
+                mm.close()
+        hub.close()
+        if errors:
+            raise errors[0]
+        calls[env] = out[0][3]
+        p = np.concatenate([s["p"] for (_, _, s, _) in out])
+        pp = np.concatenate([s["p_prime"] for (_, _, s, _) in out])
+        assert_bitwise(f"long solves [{env}]:p", p, want["p"])
+        assert_bitwise(f"long solves [{env}]:p_prime", pp, want["p_prime"])
+    # 2 steps x 21 solves of 50 sweeps: 100 calls per solve host-driven, 15
+    # with the blocks (plus the per-step u/v exchange and all-reduce)
+    assert calls["1"] * 3 <= calls["0"], calls
 
 
 @pytest.mark.parametrize("n,scheme", [(2, 1), (3, 0)])
@@ -125,7 +190,7 @@ def test_spec_slabs_rccl_loopback_fewer_collectives():
     """Two RCCL ranks (socket transport on the one GPU, tools/rccl_loopback.py)
     in the reference's tolerance mode on the channel: bitwise the single-domain
     model with the speculative slab blocks and with the host-driven loop, and
-    the blocks make a fraction of the collective calls per step."""
+    the blocks make no more collective calls per step."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from jsonl import records
     calls = {}
@@ -138,4 +203,5 @@ def test_spec_slabs_rccl_loopback_fewer_collectives():
         assert r.returncode == 0 and len(lines) == 1, (r.stdout[-2000:], r.stderr[-3000:])
         assert lines[0]["bitwise_equal_single_domain"], lines
         calls[env] = lines[0]["collective_calls_per_step_rank0"]
-    assert calls["1"] * 3 < calls["0"], calls
+    # from rest: no more calls than the host-driven loop (r6 host-side stop)
+    assert calls["1"] <= calls["0"], calls

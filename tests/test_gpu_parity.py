@@ -348,8 +348,7 @@ def test_kernel_variants_bitwise(monkeypatch, fastdiv, temporal, kind):
 
 def test_power_of_two_cavity_uses_reciprocal_multiply():
     """The bench grid proves the reciprocal multiply exact and so runs the
-    default march: kind 5 (rhs window in LDS) at 8 sweeps per launch (the
-    chained form k_jacobi_chain is opt-in, CFD_JACOBI_CHAIN=1)."""
+    default march: kind 5 (rhs window in LDS) at 8 sweeps per launch."""
     c = _cfd()
     m = c.Model(c.cavity_grid(4096), c.SimulationParams.cavity(1000.0, 200, corrector_passes=0,
                                                                tol_enabled=False))

@@ -451,10 +451,8 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     and the per-task guard falls back to the reference's form where a task
     reads a huge value: p' = 2^110 in one corner (the tiles there and those
     its values reach), rhs = 2^126 (> the 2^124 limit) in one patch (the
-    tiles that read it); distant tiles keep SUMS.  The per-launch march
-    (k_jacobi_lds, r5: the optimistic form, each wave checks its own bound
-    after its march) re-runs exactly the waves that read a huge value.  Every case bitwise vs per-launch solves in the
-    reference's form (CFD_PERSIST=0, CFD_JACOBI_SUMS=0)."""
+    tiles that read it); distant tiles keep SUMS.  Every case bitwise vs
+    per-launch solves (CFD_PERSIST=0, always the reference's form since r6)."""
     import cfdamd
     grid = cfdamd.cavity_grid(1024)
     params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
@@ -471,16 +469,10 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
     rhs_huge[500:520, 300:340] = np.float32(2.0 ** 126)
     cases = {"plain": {}, "huge_pp": {"p_prime": pp_huge.ravel()},
              "huge_rhs": {"rhs": rhs_huge.ravel()}}
-    envs = {"per_launch": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "0", "CFD_JACOBI_CHAIN": "0"},
-            "per_launch_sums": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "1", "CFD_JACOBI_CHAIN": "0"},
-            "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0", "CFD_JACOBI_CHAIN": "0"},
-            "sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "1", "CFD_JACOBI_CHAIN": "0"},
-            # r5: the chained march (default), optimistic SUMS per row group
-            "chain": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "1", "CFD_JACOBI_CHAIN": "1"}}
-    per_launch_sums = {}
+    envs = {"per_launch": {"CFD_PERSIST": "0", "CFD_JACOBI_SUMS": "0"},
+            "no_sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "0"},
+            "sums": {"CFD_PERSIST": "1", "CFD_JACOBI_SUMS": "1"}}
     sums = {}
-    chain_fb = {}
-    lds_fb = {}
     for name, inject in cases.items():
         out = {}
         for key, env in envs.items():
@@ -491,12 +483,6 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
                 mm.set_state(**dict(base, **inject))
                 mm.jacobi_pressure()
                 out[key] = (mm.get_state()["p_prime"], mm.persist_blocks, mm.persist_sums)
-                if key == "chain":
-                    cs = mm.chain_stats
-                    assert cs["launches"] == 25, cs
-                    chain_fb[name] = cs["fallbacks"]
-                if key == "per_launch_sums":
-                    lds_fb[name] = mm.chain_stats["fallbacks"]
             finally:
                 mm.close()
         for key, (pp, _, _) in out.items():
@@ -504,15 +490,6 @@ def test_persist_sums_form_runs_and_guard_falls_back(monkeypatch):
         assert out["sums"][1] == 25 and out["no_sums"][2] == 0, (out["sums"][1:], out["no_sums"][1:])
         assert out["per_launch"][1:] == (0, 0), out["per_launch"][1:]
         sums[name] = out["sums"][2]
-        per_launch_sums[name] = out["per_launch_sums"][2]
-    # per-launch march (k_jacobi_lds, r5: the optimistic form): all 25
-    # launches run it; the waves that read a huge value re-run in the
-    # reference's form, none in the plain case
-    assert per_launch_sums == {"plain": 25, "huge_pp": 25, "huge_rhs": 25}, per_launch_sums
-    assert lds_fb["plain"] == 0 and lds_fb["huge_pp"] > 0 and lds_fb["huge_rhs"] > 0, lds_fb
     # plain: the owned tiles' blocks 2..24 (blocks 0 and 1 measure the inputs)
     assert sums["plain"] > 0, sums
     assert 0 < sums["huge_pp"] < sums["plain"] and 0 < sums["huge_rhs"] < sums["plain"], sums
-    # the chain re-runs exactly the row groups that read a huge value, in the
-    # reference's form (every launch of the huge cases has some; none plain)
-    assert chain_fb["plain"] == 0 and chain_fb["huge_pp"] > 0 and chain_fb["huge_rhs"] > 0, chain_fb

@@ -184,33 +184,6 @@ def test_vector_corrector_matches_scalar(monkeypatch, grid_kind):
         assert_bitwise(f"corrector vec/scalar {grid_kind}:{f}", states[1][f], states[0][f])
 
 
-@pytest.mark.parametrize("p_tol", [1e-4, 3e-5])
-def test_spec_fold_matches_check_launch(monkeypatch, p_tol):
-    """The early-exit check folded into the speculative launch's last
-    workgroup (CFD_SPEC_FOLD=1: returning atomics, ticket, atomic-exchange
-    fold) and the default one-workgroup k_spec_check launch give the same bits
-    and sweep counts, and the folded form matches the oracle step by step."""
-    import cfdamd
-    monkeypatch.setenv("CFD_RESIDENT", "0")   # the fold belongs to the per-launch path
-    monkeypatch.setenv("CFD_SPEC_FOLD", "1")
-    params = cfdamd.SimulationParams.cavity(100.0, 50, p_tol=p_tol)
-    sweeps = _run(cfdamd.cavity_grid(128), params,
-                  dict(bc_kind=1, viscosity=0.01, p_tol=p_tol), 30, f"fold tol {p_tol}")
-    assert any(s % 8 for s in sweeps), sweeps
-    grid = cfdamd.cavity_grid(256, 128)
-    params = cfdamd.SimulationParams.cavity(400.0, 50, p_tol=2e-4)
-    states = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("CFD_SPEC_FOLD", env)
-        m = cfdamd.Model(grid, params, device=0)
-        m.update_n(15)
-        states.append(m.get_state())
-        m.close()
-    for f in STATE:
-        assert_bitwise(f"spec fold on/off:{f}", states[1][f], states[0][f])
-    assert states[0]["jacobi_sweeps_total"] == states[1]["jacobi_sweeps_total"]
-
-
 def test_resident_deadline_fault_is_loud_and_recoverable(monkeypatch):
     """A barrier wait past the deadline (forced: CFD_PERSIST_DEADLINE_US=0)
     aborts the resident solve.  r5: the model recovers by itself (checkpoint

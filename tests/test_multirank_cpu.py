@@ -332,12 +332,18 @@ def test_single_domain_blocks_split_evenly():
 # ---------------------------------------------------------------------------
 # r5: the tolerance mode on slabs as speculative T-sweep blocks
 # (enqueue_spec_slabs, cfd_model.hip; opt-in CFD_SPEC_SLABS=1).  The same
-# schedule in numpy over gloo: per block ONE p' exchange T rows deep, T sweeps
-# of the owned rows (sweep s recomputing T-1-s ghost rows each side), ONE
-# all-reduce of the block's T residuals, the first sweep below p_tol ends the
-# solve (later blocks skip); the converged block re-runs with exactly its
-# sweeps from its untouched source, the result is copied to the buffer the
-# host counted (one flip per block), and one 1-row exchange follows.
+# schedule in numpy over gloo: per block ONE p' exchange T rows deep (the
+# first block's also carries the rhs ghosts, r6), T sweeps of the owned rows
+# (sweep s recomputing T-1-s ghost rows each side), ONE all-reduce of the
+# block's T residuals, the first sweep below p_tol ends the solve (later
+# blocks skip); the converged block re-runs with exactly its sweeps from its
+# untouched source, the result is copied to the buffer the host counted (one
+# flip per block), and one 1-row exchange follows.
+# r6: the host reads each block's all-reduced residuals (block 0 at once,
+# later blocks one block behind) and enqueues no block past the one where
+# the solve ended, so the collective calls track convergence: never more than
+# the host-driven loop's 2 per enqueued sweep (it enqueues one sweep past the
+# exit), and a fraction of them when solves run long.
 
 def simd_end(nx):
     e = 1
@@ -381,15 +387,20 @@ def _spec_worker(rank, n, port, cases, results):
             bufs[0][g0:g0 + nyl] = P[j0:j1]
             rhs[g0:g0 + nyl] = RHS[j0:j1]
             exchange(bufs[0], g0, plan_halo(2, nyl, hg, rank, n), rank, n)
-            exchange(rhs, g0, plan_halo(2, nyl, hg, rank, n), rank, n)
             Tm = min(8, hg)
             nb = -(-iters // Tm)
-            it, launches, stop, collectives = 0, 0, None, 1   # the rhs exchange
+            it, launches, stop, collectives = 0, 0, None, 0
+            blk_errs, checked, host_stop = [], 0, False
             for b in range(nb):
+                if host_stop:   # the host enqueues nothing past the exit
+                    break
                 T = iters // nb + (1 if b < iters % nb else 0)
                 src = bufs[launches & 1]
+                if b == 0:   # one group: the rhs ghosts hg deep + the source T deep
+                    exchange(rhs, g0, plan_halo(2, nyl, hg, rank, n), rank, n)
                 exchange(src, g0, plan_halo(2, nyl, T, rank, n), rank, n)
-                collectives += 2
+                collectives += 2   # that exchange group + the block's all-reduce
+                errs = np.zeros(T, F)   # a skipped block publishes nothing
                 if stop is None:   # the device skips the blocks after the exit
                     res, errs = spec_block(src, rhs, g0, lo, hi, T, nx, ny, j0, dx, dy)
                     e = torch.tensor(np.array(errs, F))
@@ -402,8 +413,13 @@ def _spec_worker(rank, n, port, cases, results):
                     if hit:
                         stop = (launches, hit[0] + 1, F(errs[hit[0]]), it + hit[0] + 1)
                     last = (F(errs[-1]), it + T)
+                blk_errs.append(errs)
                 it += T
                 launches += 1
+                # the host's check: block 0 at once, later blocks one behind
+                while not host_stop and checked <= (0 if b == 0 else b - 1):
+                    host_stop = any(x < F(p_tol) for x in blk_errs[checked])
+                    checked += 1
             if stop is not None:
                 L, nsw, resid, sweeps = stop
                 src = bufs[L & 1]
@@ -502,7 +518,20 @@ def test_sharded_spec_blocks_match_single_domain(n):
         assert F(resid).view(np.uint32) == wres.view(np.uint32) and sweeps == wsweeps, \
             (nx, ny, hg, p_tol, resid, wres, sweeps, wsweeps)
         exits.add(sweeps)
-        # one exchange + one all-reduce per block, plus the rhs and final
-        # exchanges: against 2 calls per sweep for the host-driven loop
-        assert coll == 2 * -(-iters // min(8, hg)) + 2 < 2 * iters
+        # the host-driven loop (enqueue_solve_host_driven): an all-reduce and a
+        # 1-row exchange per sweep, one sweep enqueued past the exit
+        host_driven = 2 * min(sweeps + 1, iters)
+        # blocks enqueued: up to the exit's block, one more when the exit was
+        # seen one block behind (not in block 0, not in the last block)
+        Tm = min(8, hg)
+        nb = -(-iters // Tm)
+        split = [iters // nb + (1 if b < iters % nb else 0) for b in range(nb)]
+        L = next(b for b in range(nb) if sum(split[:b + 1]) >= sweeps)
+        enq = nb if F(resid) >= F(p_tol) else (1 if L == 0 else min(L + 2, nb))
+        assert coll == 2 * enq + 1, (coll, enq, sweeps)
+        assert coll <= host_driven, (coll, host_driven, sweeps)
+        if sweeps == iters:   # a full-length solve: a fraction of the calls
+            assert 2 * coll < host_driven, (coll, host_driven)
+            if Tm == 8:   # 8-sweep blocks: 15 calls against 100
+                assert 6 * coll <= host_driven, (coll, host_driven)
     assert len(exits) >= 4 and 50 in exits, sorted(exits)

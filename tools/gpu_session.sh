@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-5 GPU session runner.  Every step has its own time limit, steps are
+# GPU session runner.  Every step has its own time limit, steps are
 # chained, and the script stops at the first failure (no retries).
-#   TAG=r5a STAGES="suite smoke" tools/gpu_r5.sh
+#   TAG=r6a STAGES="suite smoke" tools/gpu_session.sh
 # Stages: suite smoke bench stats pmc ab abslab refdef parity
 # Outputs under gpurun_out/prof_$TAG.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
-TAG=${TAG:-r5}
+TAG=${TAG:-r6}
 D=gpurun_out/prof_$TAG
 mkdir -p $D
 step() {  # step <name> <seconds> <cmd...>
