@@ -226,7 +226,7 @@ void launch_lds(const Geom &g, const Fields &f, int T, int pass, int it, int par
 // below p_tol and, when it is not the launch's last, schedules the re-run
 // (launch_jacobi_redo) of that launch with exactly that many sweeps from its
 // untouched source buffer.  Later launches of the solve return at once.
-// lag > 0 (r5, one domain, CFD_SPEC_LAG=1): no k_spec_check launches -- each launch checks the
+// lag > 0 (one domain, the default since r6; CFD_SPEC_LAG=0 turns it off): no k_spec_check launches -- each launch checks the
 // previous one (lag = its sweep count) and the re-run checks the last one
 // (launch_jacobi_redo's last_*); see spec_lag_first.
 void launch_jacobi_spec(const Geom &g, const Fields &f, int pass, int it, int par, int T,

@@ -1175,9 +1175,10 @@ struct cfd_model {
                 // launch runs kSpecT sweeps with every sweep's residual, a check
                 // finds the reference's early exit (model.rs:816), and the
                 // converged launch is re-run with exactly its sweeps
-                // the check: a one-workgroup k_spec_check launch after every
-                // launch; CFD_SPEC_LAG=1 (r5) has each launch check the
-                // previous one and the re-run check the last (spec_lag_first)
+                // the check (r6 default, spec_lag_first): each launch checks
+                // the previous one and the re-run checks the last;
+                // CFD_SPEC_LAG=0: a one-workgroup k_spec_check launch after
+                // every launch
                 const bool lag = spec_lag_env;
                 int prev_T = 0, last_it = 0;
                 for (int it = 0; it < iters;) {
@@ -1471,12 +1472,14 @@ struct cfd_model {
     // blocks (enqueue_solve): per block one T-row p' exchange, one speculative
     // launch publishing every sweep's residual, one all-reduce of the block's
     // T residuals and the device-side check -- instead of a launch, a fold,
-    // an all-reduce, an exchange and a host read per sweep.  Opt-in
-    // (CFD_SPEC_SLABS=1) until it has run on the hardware
-    // (tests/test_gpu_optin_r5.py); by default the host-driven per-sweep loop.
+    // an all-reduce, an exchange and a host read per sweep.  The default
+    // since r6 (the host-side stop below): the default_grid() channel on 2
+    // RCCL ranks (loopback) 102.3 -> 33.5 ms per step, 2,102 -> 569
+    // collective calls (profiles/r6/prof_r6e/tolbench_*.log), bitwise;
+    // CFD_SPEC_SLABS=0 keeps the host-driven per-sweep loop.
     bool spec_slab_env = [] {
         const char *e = getenv("CFD_SPEC_SLABS");
-        return e && atoi(e) != 0;
+        return !(e && atoi(e) == 0);
     }();
     bool spec_slab_ok() const {
         // (k_spec_align moves float4s from pp + hg * nx: 16-B aligned rows)
@@ -1613,11 +1616,13 @@ struct cfd_model {
         const char *e = getenv("CFD_SPEC");
         return !(e && atoi(e) == 0);
     }();
-    // the lagged early-exit check (r5, spec_lag_first): opt-in (CFD_SPEC_LAG=1)
-    // until it has run on the hardware (tests/test_gpu_optin_r5.py)
+    // the lagged early-exit check (r5, spec_lag_first): the default since r6
+    // -- C3 in the reference's control flow 10.81 -> 10.50 ms per step (best
+    // of 3, medians 10.85 -> 10.53; profiles/r6/prof_r6d/ab_speclag.log);
+    // CFD_SPEC_LAG=0 keeps a k_spec_check launch after every speculative launch
     bool spec_lag_env = [] {
         const char *e = getenv("CFD_SPEC_LAG");
-        return e && atoi(e) != 0;
+        return !(e && atoi(e) == 0);
     }();
     bool spec_mode() const {
         return spec_env && !sharded() && g.tol_enabled &&
@@ -2504,11 +2509,15 @@ int create_common(const cfd_grid *grid, const cfd_params *params, int device, in
     if (n_ranks > 1) {
         // Deep halos: one RCCL round every hg sweeps (a round over xGMI is
         // latency-bound, ~20-30 us) against ~hg/nyl redundant ghost-row
-        // compute; default hg = nyl/32 clamped to [4, 32] (32 at the bench's
+        // compute; default hg = nyl/32 clamped to [8, 32] (32 at the bench's
         // 1024-2048-row slabs: 7 rounds per 200-sweep step, ~3 % extra rows).
+        // The floor 8 (r6; 4 before) lets the tolerance mode's speculative
+        // blocks run 8 sweeps per exchange on thin slabs too (the default
+        // channel on 2 ranks: 13 blocks of 4 per solve -> 7 of 8)
         uint64_t min_rows = grid->ny / (uint64_t)n_ranks;
         const char *env = getenv("CFD_HALO_DEPTH");
-        hg = env ? atoi(env) : (int)std::max<uint64_t>(4, std::min<uint64_t>(32, min_rows / 32));
+        hg = env ? atoi(env)
+                 : (int)std::max<uint64_t>(kMaxTemporal, std::min<uint64_t>(32, min_rows / 32));
         if (hg < 1) hg = 1;
         if ((uint64_t)hg + 2 > min_rows) hg = (int)(min_rows > 3 ? min_rows - 2 : 1);
         if (min_rows < 4) {

@@ -12,8 +12,9 @@ for p in (ROOT, os.path.join(ROOT, "cfd-demo_amd"), os.path.join(ROOT, "oracle")
 # bench.py self-launch).  They run after every single-process parity file, so
 # a harness fault there cannot hide the oracle checks behind it under -x (r4).
 MULTI_PROCESS_FILES = ("test_gpu_rccl.py",)
-# r5's opt-in paths not yet run on the hardware: after everything else
-LAST_FILES = ("test_gpu_optin_r5.py",)
+# r5's lagged check and speculative slab blocks (first run on the hardware in
+# r6): after everything else
+LAST_FILES = ("test_gpu_spec_lag_slabs.py",)
 
 
 def pytest_configure(config):

@@ -52,8 +52,9 @@ def _compare(tag, m, o):
 def solve_form(request, monkeypatch):
     """Every parity case runs twice: as the small-grid default, the whole
     solve in one resident launch (k_jacobi_resident), and as the per-launch
-    speculative path (CFD_RESIDENT=0: k_jacobi_lds MODE 2 + checks + redo).
-    The r5 lagged check runs the same cases in test_gpu_optin_r5.py."""
+    speculative path (CFD_RESIDENT=0: k_jacobi_lds MODE 2 with the lagged
+    check, the r6 default, + redo); test_gpu_spec_lag_slabs.py compares it
+    with the k_spec_check launches (CFD_SPEC_LAG=0)."""
     monkeypatch.setenv("CFD_RESIDENT", "1" if request.param == "resident" else "0")
     return request.param
 

@@ -1,13 +1,16 @@
-"""GPU: round-5 paths that are OPT-IN until they have run on the hardware
-(this file runs last, after the multi-process files, so a failure here cannot
-hide any default-path test under -x):
-* CFD_SPEC_LAG=1 -- the lagged early-exit check of single-domain speculative
-  solves (spec_lag_first, cfd_jacobi_lds.h): each speculative launch checks the
-  previous launch's residuals, the re-run checks the last launch's, and the
-  one-workgroup k_spec_check launches go;
+"""GPU: round-5 paths measured on the hardware in r6 (this file runs last,
+after the multi-process files, so a failure here cannot hide any default-path
+test under -x):
+* the lagged early-exit check of single-domain speculative solves
+  (spec_lag_first, cfd_jacobi_lds.h; the default since r6, CFD_SPEC_LAG=0
+  restores a k_spec_check launch after every speculative launch): each
+  speculative launch checks the previous launch's residuals, the re-run
+  checks the last launch's;
 * CFD_SPEC_SLABS=1 -- the tolerance mode on slabs as speculative T-sweep
-  blocks (enqueue_spec_slabs, cfd_model.hip) instead of the host-driven loop.
-Every case is bitwise against the oracle and against the default path."""
+  blocks (enqueue_spec_slabs, cfd_model.hip) instead of the host-driven loop,
+  stopping on the host's read of each block's all-reduced residuals (r6).
+Every case is bitwise against the oracle and against the other path.
+"""
 import os
 import subprocess
 import sys

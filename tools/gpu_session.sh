@@ -2,7 +2,7 @@
 # GPU session runner.  Every step has its own time limit, steps are
 # chained, and the script stops at the first failure (no retries).
 #   TAG=r6a STAGES="suite smoke" tools/gpu_session.sh
-# Stages: suite smoke bench stats pmc ab abslab refdef parity
+# Stages: suite tests smoke bench stats pmc pmcsq ab abvar abslab refdef parity
 # Outputs under gpurun_out/prof_$TAG.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
@@ -54,6 +54,10 @@ fi
 if has ab; then
   # AB_SETTINGS: space-separated env settings ("" = default), e.g. "'' CFD_X=1"
   step ab_${AB_NAME:-x} ${AB_SECS:-500} env AB_ROUNDS=${AB_ROUNDS:-3} AB_CMD="${AB_CMD:-tb_one.py 4096 5}" TB_WARMUP=${TB_WARMUP:-200} python3 -u tools/ab_env.py ${AB_SETTINGS}
+fi
+if has abvar; then
+  # AB_VARIANTS: libraries built by tools/build_variants.sh (lib/variants/<name>)
+  step abvar_${AB_NAME:-x} ${AB_SECS:-500} env AB_ROUNDS=${AB_ROUNDS:-3} AB_CMD="${AB_CMD:-tb_one.py 4096 5}" TB_WARMUP=${TB_WARMUP:-200} python3 -u tools/ab_variants.py ${AB_VARIANTS}
 fi
 if has abslab; then
   # persistent vs per-launch on the exact rank geometries (tb_one slab proxies

@@ -35,7 +35,8 @@ base = t0.min()
 st = (t0 - base) * 10.0 / 1000.0     # us (100 MHz)
 en = (t1 - base) * 10.0 / 1000.0
 life = en - st
-clk = s[:, 2].astype(np.float64) / np.maximum(life, 1e-3) / 1e3   # GHz
+clk = (s[:, 2] & 0xFFFFFFFFFF).astype(np.float64) / np.maximum(life, 1e-3) / 1e3   # GHz
+bid = (s[:, 2] >> 40).astype(np.int64)
 hw = (s[:, 3] & 0xFFFFFFFF).astype(np.int64)
 xcc = (s[:, 3] >> 32).astype(np.int64) & 0xF
 simd = (hw >> 4) & 3
@@ -52,6 +53,36 @@ out = {"waves": int(len(s)), "span_us": round(float(en.max()), 2),
        "waves_per_cu_hist": dict(sorted(collections.Counter(per_cu.values()).items())),
        "waves_per_simd_hist": dict(sorted(collections.Counter(per_simd.values()).items())),
        "kernel": m.kernel_config}
+# which waves end last: the wave's (column, segment) from its XCD-renumbered
+# block and wave index (the stamp's slot is blockIdx * 4 + wave, in order)
+geo = m.jacobi_geometry(False)
+nwc, nseg = geo["wave_cols"], geo["segments"]
+slot = np.nonzero(buf[: got * 4].reshape(-1, 4)[:, 1] > 0)[0]
+wave = slot % 4
+if len(s) > nwc * nseg:   # the filled round (lds_fill_waves)
+    wtot = len(s)
+    gw = bid * 4 + wave
+    q_, rem = wtot // nwc, wtot % nwc
+    big = rem * (q_ + 1)
+    wc = np.where(gw < big, gw // (q_ + 1), rem + (gw - big) // max(q_, 1))
+    seg = np.where(gw < big, gw - wc * (q_ + 1), gw - big - (wc - rem) * q_)
+    ns = np.where(wc < rem, q_ + 1, q_)
+else:
+    wc = bid % nwc
+    seg = (bid // nwc) * 4 + wave
+    ns = np.full_like(seg, nseg)
+row_edge = (seg == 0) | (seg == ns - 1)
+col_edge = (wc == 0) | (wc == nwc - 1)
+simd_load = np.array([per_simd[k] for k in (cukey * 4 + simd).tolist()])
+cats = {"interior": ~row_edge & ~col_edge, "row_edge": row_edge & ~col_edge,
+        "col_edge": col_edge & ~row_edge, "corner": row_edge & col_edge}
+for w_ in sorted(set(simd_load.tolist())):
+    cats[f"simd_{w_}_waves"] = simd_load == w_
+for par in (0, 1):
+    cats[f"seg_parity_{par}"] = (seg % 2 == par) & ~row_edge & ~col_edge
+last = en >= np.percentile(en, 95)
+out["by_kind"] = {k: {"n": int(v.sum()), "end_us_pct": q(en[v]) if v.any() else None,
+                      "in_last_5pct": int((v & last).sum())} for k, v in cats.items()}
 # time histogram of live waves (10 bins over the span)
 edges = np.linspace(0, en.max(), 11)
 out["live_waves_at"] = [int(((st <= x) & (en > x)).sum()) for x in (edges[:-1] + edges[1:]) / 2]

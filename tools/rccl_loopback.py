@@ -84,6 +84,9 @@ def worker(args):
     if args.mode == "developed":
         developed(args, rank, n, cfdamd, dist, np)
         return
+    if args.mode == "tolbench":
+        tolbench(args, rank, n, cfdamd, dist, np)
+        return
     report = []
     for name, grid, params in cases:
         if rank == 0:
@@ -219,6 +222,58 @@ def developed(args, rank, n, cfdamd, dist, np):
         sys.exit(1)
 
 
+def tolbench(args, rank, n, cfdamd, dist, np):
+    """The reference's design point in its own control flow on slabs: the
+    default_grid() channel (800 x 264, cylinder, SimulationParams::default():
+    <= 50 sweeps, early exit 1e-4, <= 20 corrector passes), --develop steps
+    from rest untimed, then --steps steps timed: wall ms and collective calls
+    per step, and the state after them bit for bit against the single-domain
+    model.  Run once per solve schedule (CFD_SPEC_SLABS=0: the host-driven
+    per-sweep loop; 1: the speculative blocks)."""
+    grid = cfdamd.default_grid()
+    params = cfdamd.SimulationParams()
+    obj = [cfdamd.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=rank, unique_id=obj[0])
+    m.update_n(args.develop)
+    m.synchronize()
+    dist.barrier()
+    c0 = m.comm_calls
+    s0 = m.get_residuals().jacobi_sweeps_total
+    t0 = time.perf_counter()
+    m.update_n(args.steps)
+    m.synchronize()
+    el = time.perf_counter() - t0
+    calls = (m.comm_calls - c0) / args.steps
+    sweeps = (m.get_residuals().jacobi_sweeps_total - s0) / args.steps
+    st = m.get_state()
+    mine = (m.j0, m.j1, {k: st[k] for k in ("u", "p", "p_prime")})
+    m.close()
+    gathered = [None] * n
+    dist.all_gather_object(gathered, (mine, el))
+    if rank == 0:
+        ref = cfdamd.Model(grid, params, device=0)
+        ref.update_n(args.develop + args.steps)
+        want = ref.get_state()
+        ref.close()
+        ok = all(np.array_equal(np.concatenate([g[0][2][k] for g in gathered]).view(np.uint32),
+                                want[k].view(np.uint32)) for k in ("u", "p", "p_prime"))
+        wall = max(g[1] for g in gathered)
+        result(args, rank, {"case": "default_grid() channel, reference control flow",
+                            "schedule": "speculative blocks" if os.environ.get("CFD_SPEC_SLABS") == "1"
+                            else "host-driven per sweep",
+                            "ranks": n, "develop": args.develop, "steps": args.steps,
+                            "ms_per_step": 1e3 * wall / args.steps,
+                            "collective_calls_per_step_rank0": calls,
+                            "ms_per_collective_call": 1e3 * wall / args.steps / max(calls, 1e-9),
+                            "sweeps_per_step": sweeps,
+                            "bitwise_equal_single_domain": bool(ok)})
+        if not ok:
+            sys.exit(1)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=2)
@@ -226,7 +281,7 @@ def main():
     ap.add_argument("--ny", type=int, default=200)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--mode", default="both",
-                    choices=["fixed", "tol", "both", "solvers", "developed", "selftest"])
+                    choices=["fixed", "tol", "both", "solvers", "developed", "tolbench", "selftest"])
     ap.add_argument("--develop", type=int, default=400)
     ap.add_argument("--timeout", type=float, default=240.0)
     ap.add_argument("--lines", type=int, default=200)
