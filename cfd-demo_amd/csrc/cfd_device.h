@@ -81,7 +81,8 @@ __device__ __forceinline__ float from_right(float x) {
 // FAST 3 (r4): the FMA-corrected form for |x| >= 2^-96 and IEEE `/` below
 // (where the correction's residual underflows: every mismatch of form 2 on
 // the reference's default-grid divisors lies at |x| < 2^-104), proven for all
-// 2^32 inputs per divisor like the others; NaN takes the IEEE branch.
+// 2^32 inputs per divisor like the others; NaN takes the IEEE branch, +-0 the
+// product (r6).
 constexpr float kDivGuardMin = 0x1p-96f;
 template <int FAST>
 __device__ __forceinline__ float fdiv(float x, float c, float r) {
@@ -92,10 +93,13 @@ __device__ __forceinline__ float fdiv(float x, float c, float r) {
         return __builtin_isfinite(q0) ? q : q0;
     }
     if (FAST == 3) {
-        if (__builtin_expect(__builtin_fabsf(x) >= kDivGuardMin, 1)) {
+        // (r6) a zero dividend takes the product too: x * r is +-0 with x's
+        // sign, as x / c -- exact zeros (a cold or Dirichlet region) no longer
+        // send the wave down the IEEE branch; proven with the rest
+        if (__builtin_expect(__builtin_fabsf(x) >= kDivGuardMin || x == 0.0f, 1)) {
             const float q0 = x * r;
             const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
-            return __builtin_isfinite(q0) ? q : q0;
+            return __builtin_isfinite(q0) && x != 0.0f ? q : q0;
         }
     }
     return x / c;

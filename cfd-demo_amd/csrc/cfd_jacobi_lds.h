@@ -441,7 +441,7 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
                                           float *__restrict__ pb, const float *__restrict__ rhs,
                                           Ctl *ctl, uint32_t *res_slots, int par, int out_lo,
                                           int out_hi, int nwc, int nseg, int wlo, int whi, f2 *lds,
-                                          int nst, int bid, float *trk = nullptr, int wtot = 0) {
+                                          int nst, int bid, float *trk = nullptr) {
     using M = LdsMarch<T, FAST, MODE, SUMS>;
     constexpr bool RES = M::RES;
     M w;
@@ -449,28 +449,8 @@ __device__ __forceinline__ void lds_block(const Geom &g, float *__restrict__ pa,
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int lane = (int)threadIdx.x & 63;
     if (M::PERSIST && trk && lane == 0) trk[3 * wave] = trk[3 * wave + 1] = trk[3 * wave + 2] = 0.0f;
-    int wc, seg;
-    if (wtot > 0) {
-        // r6, one filled round (lds_fill_waves): the launch's wtot waves in
-        // order, column by column, the first wtot % nwc columns one segment
-        // more -- every slot of the round holds a wave, not just whole
-        // 4-segment groups per column (740 of 768 workgroup slots at 4096^2)
-        const int gw = bid * kLdsWaves + wave;
-        if (gw >= wtot) return;
-        const int q = wtot / nwc, rem = wtot % nwc, big = rem * (q + 1);
-        if (gw < big) {
-            wc = gw / (q + 1);
-            seg = gw - wc * (q + 1);
-            nseg = q + 1;
-        } else {
-            wc = rem + (gw - big) / q;
-            seg = gw - big - (wc - rem) * q;
-            nseg = q;
-        }
-    } else {
-        wc = bid % nwc;
-        seg = (bid / nwc) * kLdsWaves + wave;
-    }
+    const int wc = bid % nwc;
+    const int seg = (bid / nwc) * kLdsWaves + wave;
     const int nrows = out_hi - out_lo;
     if (seg >= nseg) return;
     // rows split in proportion to weights: 16 per segment, wlo / whi for the
@@ -637,7 +617,7 @@ template <int T, int FAST, int MODE>
 __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_lds(
     Geom g, float *__restrict__ pa, float *__restrict__ pb, const float *__restrict__ rhs,
     Ctl *ctl, uint32_t *res_slots, int pass, int par, int out_lo, int out_hi, int nwc, int nseg,
-    int wlo, int whi, int it, int lag, int wtot) {
+    int wlo, int whi, int it, int lag) {
     using M = LdsMarch<T, FAST, MODE>;
     [[maybe_unused]] constexpr bool RES = M::RES;   // the stamp guard's
     __shared__ f2 lds[kLdsWaves * M::D * 64];
@@ -697,7 +677,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
         if (nst <= 0) return;
     }
     lds_block<T, FAST, MODE>(g, pa, pb, rhs, ctl, res_slots, par, out_lo, out_hi, nwc, nseg, wlo,
-                             whi, lds, nst, xcd_block(g), nullptr, wtot);
+                             whi, lds, nst, xcd_block(g));
 }
 
 // Persistent fixed-count solve: ONE launch runs nblk blocks of T sweeps
@@ -1098,35 +1078,6 @@ int lds_segments(const Geom &g, int nrows, int nwc, int pad, int occ_override = 
     return std::max(1, std::min(per_round * rounds, nrows / kMinRows));
 }
 
-// r6: waves of ONE filled round of the launch (lds_block's wtot), or 0 for
-// whole 4-segment groups per wave column.  The per-column layout leaves
-// n_cu * occ - nwc * ceil(nseg / 4) workgroup slots empty (4096^2: 740 of
-// 768, 28 CUs at 2 workgroups finishing early) while every other wave
-// marches the full segment; filling the round spreads the rows over all
-// n_cu * occ * 4 waves (each column floor or ceil of wtot / nwc segments).
-// Only where the per-column layout is itself one round of segments of at
-// least kMinRows rows; CFD_LDS_FILL=0 keeps the per-column layout.
-template <int T, int FAST, int MODE>
-int lds_fill_waves(const Geom &g, int nrows, int nwc, int nseg, int pad) {
-    static const int env = [] {
-        const char *e = getenv("CFD_LDS_FILL");
-        return e ? atoi(e) : 1;
-    }();
-    if (!env || g.tb_rows > 0) return 0;
-    static const int bpc_cap = [] {
-        const char *e = getenv("CFD_LDS_BPC");
-        return e ? std::max(1, atoi(e)) : 0;
-    }();
-    const int occ = lds_blocks_per_cu<T, FAST, MODE>(pad);
-    const int bpc = bpc_cap > 0 ? std::min(occ, bpc_cap) : occ;
-    const int wtot = kLdsWaves * g.n_cu * bpc;
-    // the per-column layout's round must be the whole launch, and the filled
-    // layout's shortest segments long enough
-    if (nwc * cdiv(nseg, kLdsWaves) > g.n_cu * bpc || wtot <= nwc * nseg) return 0;
-    if (nrows / cdiv(wtot, nwc) < 8) return 0;
-    return wtot;
-}
-
 template <int T, int MODE>
 void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int out_lo, int out_hi,
                   uint32_t *rs, hipStream_t s, int lag = 0) {
@@ -1137,11 +1088,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int nseg = g.fastdiv == 1   ? lds_segments<T, 1, MODE>(g, nrows, nwc, pad)
                      : g.fastdiv == 2 ? lds_segments<T, 2, MODE>(g, nrows, nwc, pad)
                                       : lds_segments<T, 0, MODE>(g, nrows, nwc, pad);
-    const int wtot = g.fastdiv == 1   ? lds_fill_waves<T, 1, MODE>(g, nrows, nwc, nseg, pad)
-                     : g.fastdiv == 2 ? lds_fill_waves<T, 2, MODE>(g, nrows, nwc, nseg, pad)
-                                      : lds_fill_waves<T, 0, MODE>(g, nrows, nwc, nseg, pad);
-    const dim3 grid(wtot > 0 ? cdiv(wtot, kLdsWaves) : nwc * cdiv(nseg, kLdsWaves)),
-        block(kLdsWaves * 64);
+    const dim3 grid(nwc * cdiv(nseg, kLdsWaves)), block(kLdsWaves * 64);
     float *pa = f.pp[0] - (long)g.hg * g.nx, *pb = f.pp[1] - (long)g.hg * g.nx;
     // a segment whose rows reach a global boundary row runs the kCol|kRow
     // path, ~1.45x the VALU work per row of an interior one (r2 wave
@@ -1152,7 +1099,7 @@ void launch_lds_t(const Geom &g, const Fields &f, int pass, int par, int it, int
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
 #define CFD_LDS_LAUNCH(FASTV)                                                                      \
     hipLaunchKernelGGL((k_jacobi_lds<T, FASTV, MODE>), grid, block, pad, s, g, pa, pb, f.rhs, f.ctl, \
-                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, lag, wtot)
+                       rs, pass, par, out_lo, out_hi, nwc, nseg, wlo, whi, it, lag)
     if (g.fastdiv == 1)
         CFD_LDS_LAUNCH(1);
     else if (g.fastdiv == 2)

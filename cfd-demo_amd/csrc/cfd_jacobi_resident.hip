@@ -382,10 +382,13 @@ inline int resident_waves() {
     return e && atoi(e) == 16 ? 16 : 8;
 }
 
+// rows per thread step: 1 by default since r6 (with the r6 tile candidates:
+// the reference default 3.60 -> 3.23 ms per step at 18 x 48 tiles, against
+// 3.33 with 2 rows, profiles/r6/prof_r6j/ab_refdef3.log); CFD_RESIDENT_ROWS=2 / 4
 inline int resident_rows() {
     const char *re = getenv("CFD_RESIDENT_ROWS");
-    const int r = re ? atoi(re) : 2;
-    return r == 1 || r == 4 ? r : 2;
+    const int r = re ? atoi(re) : 1;
+    return r == 2 || r == 4 ? r : 1;
 }
 
 // Workgroups of the instantiation that will be launched (waves, rows per
@@ -427,8 +430,12 @@ inline int resident_gpc() {
 bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
     if (g.nx < 4 || g.ny < 4 || g.j0 != 0 || g.nyl != g.ny) return false;
     // box widths BC + 2e (e = 0..T-1) fill 64-lane passes: BC = 48 -> 48..62
-    // columns in one pass, 112 -> 112..126 in two
-    static const int cand[][2] = {{8, 48}, {16, 48}, {32, 48}, {16, 112}, {32, 112}};
+    // columns in one pass, 112 -> 112..126 in two.  r6: rows 18-24 too -- the
+    // reference default (800 x 264) took 32 x 48 (153 tiles, box 48 x 64);
+    // 18 x 48 (255 tiles, box 34 x 64) runs the step 3.60 -> 3.23 ms
+    // (profiles/r6/prof_r6i, prof_r6j)
+    static const int cand[][2] = {{8, 48},  {16, 48},  {18, 48},  {20, 48},
+                                  {24, 48}, {32, 48},  {16, 112}, {32, 112}};
     const int gpc = resident_gpc();
     long best = -1;
     for (const auto &cd : cand) {
