@@ -95,12 +95,17 @@ __device__ __forceinline__ float fdiv(float x, float c, float r) {
     if (FAST == 3) {
         // (r6) a zero dividend takes the product too: x * r is +-0 with x's
         // sign, as x / c -- exact zeros (a cold or Dirichlet region) no longer
-        // send the wave down the IEEE branch; proven with the rest
-        if (__builtin_expect(__builtin_fabsf(x) >= kDivGuardMin || x == 0.0f, 1)) {
-            const float q0 = x * r;
-            const float q = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
-            return __builtin_isfinite(q0) && x != 0.0f ? q : q0;
-        }
+        // need the IEEE division; and the guard is ONE wave-uniform branch:
+        // the corrected product for every lane, the IEEE quotient only when
+        // some lane of the wave needs it (no per-lane exec-mask juggling per
+        // division).  Each lane's value is the same function of x as before,
+        // so the exhaustive per-divisor proof (k_verify_division) covers it.
+        const float q0 = x * r;
+        const float qc = __builtin_fmaf(__builtin_fmaf(-q0, c, x), r, q0);
+        float q = __builtin_isfinite(q0) && x != 0.0f ? qc : q0;
+        const bool ok = __builtin_fabsf(x) >= kDivGuardMin || x == 0.0f;   // NaN: not ok
+        if (__builtin_expect(!__all(ok), 0)) q = ok ? q : x / c;
+        return q;
     }
     return x / c;
 }
