@@ -673,8 +673,13 @@ __global__ __launch_bounds__(kJacWavesPerBlock * 64) void k_jacobi(
     if (lane == 0) publish_max(slots + (size_t)it * kResSlots * kResStride, bid * kJacWavesPerBlock + wave, m);
 }
 
-// (solve_finalize_body: cfd_device.h, shared with the resident solve)
-__global__ __launch_bounds__(kBlock) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
+// (solve_finalize_body: cfd_device.h, shared with the resident solve).
+// r6: 1,024 threads -- a tolerance-mode solve's finalize folds and clears
+// every sweep's 32 residual slots (50 sets), one set per wave at a time: 16
+// waves take 4 rounds of slot reads instead of 13 (C3 in the reference's
+// control flow spent 12.9 us per solve here, 21 solves per step).
+constexpr int kFinThreads = 1024;
+__global__ __launch_bounds__(kFinThreads) void k_finalize_solve(Geom g, Fields f, int pass, int iters,
                                                            int check_break, int flips,
                                                            int exact_flips) {
     solve_finalize_body(g, f, pass, iters, check_break, flips, exact_flips);
@@ -870,7 +875,14 @@ __device__ __forceinline__ float u_corr(const Geom &g, float us, float pr, float
                          : us - dt * sdiv<SP>(pr - pw, g.dx, g.r_dx);
 }
 
-template <int SP>
+// ROWS allocation rows per thread (r6: a band march of kCfRows rows, as
+// k_correct_finish4m): row lr's p' row, its v correction and the p' row below
+// it come from row lr-1's iteration -- the v_row of row lr+1 that the
+// divergence needs is the next row's vlo, the p' row lr+1 it loads the next
+// row's pc -- instead of every row re-reading three p' rows and two v* rows
+// and computing two v rows.  The same expressions on the same inputs: bitwise
+// the one-row form (ROWS = 1).
+template <int SP, int ROWS>
 __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int pass,
                                                           float dt_override, int nbx, int has_next) {
     Ctl *c = f.ctl;
@@ -884,28 +896,10 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
     float *__restrict__ out_v = odd ? f.v_star : f.v;
     const int bid = xcd_block(g);
     const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
-    const int lr = bid / nbx - kGhostUV;   // allocation row: v rows -G..nyl+G, u rows -G..nyl+G-1
     const int nx = g.nx, W = nx + 1, nyl = g.nyl;
     if (i0 >= nx) return;
     const float dt = dt_of(c, dt_override);
     const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
-    const long kc = (long)lr * nx + i0, ku = (long)lr * W + i0;
-    const bool owned = lr >= 0 && lr < nyl;
-    // u* <- u and v* <- v of the whole row (the next pass's u* at places no
-    // corrector writes, or the last odd pass's u*): only when u* is out of date
-    if (odd && (!head || !owned)) {
-        *reinterpret_cast<float4 *>(f.v_star + kc) = *reinterpret_cast<const float4 *>(f.v + kc);
-        if (lr < nyl + kGhostUV) {   // not v's extra face row
-            const float *__restrict__ ur = f.u + ku;
-            float *__restrict__ us = f.u_star + ku;
-            us[0] = ur[0];
-            us[1] = ur[1];
-            us[2] = ur[2];
-            us[3] = ur[3];
-            if (i0 + 4 == nx) us[4] = ur[4];   // face nx
-        }
-    }
-    if (!owned && (head || lr != nyl)) return;
     auto v_row = [&](int r, const float4 &pt, bool *hit) -> float4 {
         const int jr = g.j0 + r;
         const long k = (long)r * nx + i0;
@@ -920,69 +914,100 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
         o.w = vs.w - dt * sdiv<SP>(pt.w - pb.w, g.dy, g.r_dy);
         return o;
     };
-    if (!head) {
-        // the loop's last corrector: u, v, p final (rows 0..nyl; v's row nyl)
-        float4 pc = {0.f, 0.f, 0.f, 0.f};
-        if (owned) {
-            pc = *reinterpret_cast<const float4 *>(pp + kc);
-            const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
-            const float pr[4] = {pc.x, pc.y, pc.z, pc.w};
-            const float pw[4] = {pl, pc.x, pc.y, pc.z};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int i = i0 + q;
-                if (i < 1 || i > nx - 1) continue;
-                f.u[ku + q] = u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i);
+    // allocation rows: v rows -G..nyl+G, u rows -G..nyl+G-1
+    const int lr0 = (bid / nbx) * ROWS - kGhostUV, lr1 = min(lr0 + ROWS, nyl + 1 + kGhostUV);
+    bool carry = false;          // p' row lr and v row lr from row lr-1's iteration
+    float4 p_next = {0.f, 0.f, 0.f, 0.f}, v_next = {0.f, 0.f, 0.f, 0.f};
+    for (int lr = lr0; lr < lr1; ++lr) {
+        const long kc = (long)lr * nx + i0, ku = (long)lr * W + i0;
+        const bool owned = lr >= 0 && lr < nyl;
+        // u* <- u and v* <- v of the whole row (the next pass's u* at places no
+        // corrector writes, or the last odd pass's u*): only when u* is out of date
+        if (odd && (!head || !owned)) {
+            *reinterpret_cast<float4 *>(f.v_star + kc) = *reinterpret_cast<const float4 *>(f.v + kc);
+            if (lr < nyl + kGhostUV) {   // not v's extra face row
+                const float *__restrict__ ur = f.u + ku;
+                float *__restrict__ us = f.u_star + ku;
+                us[0] = ur[0];
+                us[1] = ur[1];
+                us[2] = ur[2];
+                us[3] = ur[3];
+                if (i0 + 4 == nx) us[4] = ur[4];   // face nx
             }
         }
-        bool hit;
-        const float4 o = v_row(lr, owned ? pc : *reinterpret_cast<const float4 *>(pp + kc), &hit);
-        if (hit) *reinterpret_cast<float4 *>(f.v + kc) = o;
-        if (owned) {
-            float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
-            pv.x = pv.x + pc.x;
-            pv.y = pv.y + pc.y;
-            pv.z = pv.z + pc.z;
-            pv.w = pv.w + pc.w;
-            *reinterpret_cast<float4 *>(f.p + kc) = pv;
+        if (!owned && (head || lr != nyl)) {
+            carry = false;
+            continue;
         }
-        return;
-    }
-    // ---- an owned row: corrector k, then pass k+1's copy and divergence
-    const float4 pc = *reinterpret_cast<const float4 *>(pp + kc);
-    const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
-    const float p4 = i0 + 4 < nx ? pp[kc + 4] : 0.0f;   // for the east face i0+4
-    const float pr[5] = {pc.x, pc.y, pc.z, pc.w, p4};
-    const float pw[5] = {pl, pc.x, pc.y, pc.z, pc.w};
-    float un[5];
+        if (!head) {
+            // the loop's last corrector: u, v, p final (rows 0..nyl; v's row nyl)
+            float4 pc = {0.f, 0.f, 0.f, 0.f};
+            if (owned) {
+                pc = *reinterpret_cast<const float4 *>(pp + kc);
+                const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
+                const float pr[4] = {pc.x, pc.y, pc.z, pc.w};
+                const float pw[4] = {pl, pc.x, pc.y, pc.z};
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        const int i = i0 + q;
-        un[q] = (i >= 1 && i <= nx - 1) ? u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i)
-                                        : f.u[ku + q];   // faces 0 and nx keep u
+                for (int q = 0; q < 4; ++q) {
+                    const int i = i0 + q;
+                    if (i < 1 || i > nx - 1) continue;
+                    f.u[ku + q] = u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i);
+                }
+            }
+            bool hit;
+            const float4 o = v_row(lr, owned ? pc : *reinterpret_cast<const float4 *>(pp + kc), &hit);
+            if (hit) *reinterpret_cast<float4 *>(f.v + kc) = o;
+            if (owned) {
+                float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
+                pv.x = pv.x + pc.x;
+                pv.y = pv.y + pc.y;
+                pv.z = pv.z + pc.z;
+                pv.w = pv.w + pc.w;
+                *reinterpret_cast<float4 *>(f.p + kc) = pv;
+            }
+            carry = false;
+            continue;
+        }
+        // ---- an owned row: corrector k, then pass k+1's copy and divergence
+        const float4 pc = carry ? p_next : *reinterpret_cast<const float4 *>(pp + kc);
+        const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
+        const float p4 = i0 + 4 < nx ? pp[kc + 4] : 0.0f;   // for the east face i0+4
+        const float pr[5] = {pc.x, pc.y, pc.z, pc.w, p4};
+        const float pw[5] = {pl, pc.x, pc.y, pc.z, pc.w};
+        float un[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const int i = i0 + q;
+            un[q] = (i >= 1 && i <= nx - 1) ? u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i)
+                                            : f.u[ku + q];   // faces 0 and nx keep u
+        }
+        out_u[ku] = un[0];
+        out_u[ku + 1] = un[1];
+        out_u[ku + 2] = un[2];
+        out_u[ku + 3] = un[3];
+        if (i0 + 4 == nx) out_u[ku + 4] = un[4];
+        bool hit;
+        const float4 vlo = carry ? v_next : v_row(lr, pc, &hit);
+        const float4 pt = *reinterpret_cast<const float4 *>(pp + kc + nx);
+        const float4 vhi = v_row(lr + 1, pt, &hit);
+        *reinterpret_cast<float4 *>(out_v + kc) = vlo;
+        float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
+        pv.x = pv.x + pc.x;
+        pv.y = pv.y + pc.y;
+        pv.z = pv.z + pc.z;
+        pv.w = pv.w + pc.w;
+        *reinterpret_cast<float4 *>(f.p + kc) = pv;
+        const float rdx = g.r_dx, rdy = g.r_dy, dx = g.dx, dy = g.dy;
+        float4 r;   // k_divergence's expression on the new u*, v*
+        r.x = (sdiv<SP>(un[1] - un[0], dx, rdx) + sdiv<SP>(vhi.x - vlo.x, dy, rdy)) / dt;
+        r.y = (sdiv<SP>(un[2] - un[1], dx, rdx) + sdiv<SP>(vhi.y - vlo.y, dy, rdy)) / dt;
+        r.z = (sdiv<SP>(un[3] - un[2], dx, rdx) + sdiv<SP>(vhi.z - vlo.z, dy, rdy)) / dt;
+        r.w = (sdiv<SP>(un[4] - un[3], dx, rdx) + sdiv<SP>(vhi.w - vlo.w, dy, rdy)) / dt;
+        *reinterpret_cast<float4 *>(f.rhs + kc) = r;
+        carry = ROWS > 1;
+        p_next = pt;
+        v_next = vhi;
     }
-    out_u[ku] = un[0];
-    out_u[ku + 1] = un[1];
-    out_u[ku + 2] = un[2];
-    out_u[ku + 3] = un[3];
-    if (i0 + 4 == nx) out_u[ku + 4] = un[4];
-    bool hit;
-    const float4 vlo = v_row(lr, pc, &hit);
-    const float4 vhi = v_row(lr + 1, *reinterpret_cast<const float4 *>(pp + kc + nx), &hit);
-    *reinterpret_cast<float4 *>(out_v + kc) = vlo;
-    float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
-    pv.x = pv.x + pc.x;
-    pv.y = pv.y + pc.y;
-    pv.z = pv.z + pc.z;
-    pv.w = pv.w + pc.w;
-    *reinterpret_cast<float4 *>(f.p + kc) = pv;
-    const float rdx = g.r_dx, rdy = g.r_dy, dx = g.dx, dy = g.dy;
-    float4 r;   // k_divergence's expression on the new u*, v*
-    r.x = (sdiv<SP>(un[1] - un[0], dx, rdx) + sdiv<SP>(vhi.x - vlo.x, dy, rdy)) / dt;
-    r.y = (sdiv<SP>(un[2] - un[1], dx, rdx) + sdiv<SP>(vhi.y - vlo.y, dy, rdy)) / dt;
-    r.z = (sdiv<SP>(un[3] - un[2], dx, rdx) + sdiv<SP>(vhi.z - vlo.z, dy, rdy)) / dt;
-    r.w = (sdiv<SP>(un[4] - un[3], dx, rdx) + sdiv<SP>(vhi.w - vlo.w, dy, rdy)) / dt;
-    *reinterpret_cast<float4 *>(f.rhs + kc) = r;
 }
 
 // ------------------------------------------------- velocity boundaries (K6)
@@ -1710,7 +1735,7 @@ void launch_verify_division(float c, float r, unsigned long long *dev_counts, hi
 
 void launch_finalize_solve(const Geom &g, const Fields &f, int pass, int iters, int check_break,
                            int flips, hipStream_t s, int exact_flips) {
-    hipLaunchKernelGGL(k_finalize_solve, dim3(1), dim3(kBlock), 0, s, g, f, pass, iters,
+    hipLaunchKernelGGL(k_finalize_solve, dim3(1), dim3(kFinThreads), 0, s, g, f, pass, iters,
                        check_break, flips, exact_flips);
 }
 
@@ -1749,12 +1774,16 @@ bool correct_head_ok(const Geom &g, const Fields &f) {
 void launch_correct_head(const Geom &g, const Fields &f, int pass, float dt_override, bool has_next,
                          hipStream_t s) {
     const int nbx4 = cdiv(g.nx / 4, kBlock);
-    const dim3 grid(nbx4 * (g.nyl + 1 + 2 * kGhostUV));
     const int hn = has_next ? 1 : 0;
-    if (g.sp_pow2)
-        hipLaunchKernelGGL(k_correct_head4<1>, grid, dim3(kBlock), 0, s, g, f, pass, dt_override, nbx4, hn);
-    else
-        hipLaunchKernelGGL(k_correct_head4<0>, grid, dim3(kBlock), 0, s, g, f, pass, dt_override, nbx4, hn);
+    // the band march, kCfRows rows per thread (r6: C3 in the reference's control
+    // flow 10.37 -> 10.26 ms per step against one row per thread, best of 3;
+    // profiles/r6/prof_r6p/ab_corrhead.log)
+    const dim3 grid(nbx4 * cdiv(g.nyl + 1 + 2 * kGhostUV, kCfRows));
+#define CFD_LAUNCH_CH(SPV, RW)                                                                    \
+    hipLaunchKernelGGL((k_correct_head4<SPV, RW>), grid, dim3(kBlock), 0, s, g, f, pass, dt_override, \
+                       nbx4, hn)
+    if (g.sp_pow2) CFD_LAUNCH_CH(1, kCfRows); else CFD_LAUNCH_CH(0, kCfRows);
+#undef CFD_LAUNCH_CH
 }
 
 bool correct_finish_folds_finalize(const Geom &g, const Fields &f) {
