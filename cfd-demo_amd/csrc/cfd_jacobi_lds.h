@@ -43,9 +43,17 @@ constexpr int kLdsWaves = 4;   // waves per workgroup (256 threads)
 #ifndef CFD_LDS_PD
 #define CFD_LDS_PD 3   // prefetch distance (slots) of the p' and rhs rows
 #endif
-// CFD_LDS_DIAG (timing diagnostics only, WRONG results): 1 = no global loads
-// (rows are a lane constant), 2 = no LDS ring (stage s reads the register
-// prefetch of another row), 3 = both
+// CFD_LDS_DIAG (timing diagnostics only, WRONG results), bits: 1 = no global
+// loads (rows are a lane constant), 2 = no LDS ring (stage s reads the
+// register prefetch of another row), 4 = no p' stores.  At 4096^2 (r6,
+// profiles/r6/prof_r6q/abvar_diag.log): 5.03 us per sweep; without stores
+// 4.46, without loads 4.15, without both 4.06.  gfx950 counts a wave's loads
+// and stores in ONE vmcnt, in issue order, so each wait for a prefetched row
+// also waits for the p' stores issued before it: the stores cost through that
+// coupling.  A fifth "store wave" per workgroup draining LDS rings of the
+// output rows measured slower (5.79; 5.22 even with its stores and ring waits
+// compiled out -- the 96-VGPR cap that 5 waves per SIMD need, and the fifth
+// wave shares wave 0's SIMD: profiles/r6/prof_r6t, prof_r6s/wave_place.log).
 #ifndef CFD_LDS_DIAG
 #define CFD_LDS_DIAG 0
 #endif
@@ -205,6 +213,10 @@ struct LdsMarch {
         return (f2){__uint_as_float(v.x), __uint_as_float(v.y)};
     }
     __device__ __forceinline__ void st(const f2 &x, int row) const {
+        if (CFD_LDS_DIAG & 4) {   // keep the value live without storing it
+            asm volatile("" ::"v"(x.x), "v"(x.y));
+            return;
+        }
         const u32x2 v = {__float_as_uint(x.x), __float_as_uint(x.y)};
         __builtin_amdgcn_raw_buffer_store_b64(v, rs_d, vo_st, (row - wbase) * row_bytes, PST_AUX);
     }
