@@ -114,7 +114,6 @@ struct Geom {
                           // 3: 4 columns per lane, 4: 2 columns per lane; 5: the
                           // 2-column march with its rhs window in LDS
     int32_t xcd_remap;    // renumber blocks so each XCD gets contiguous tiles (xcd_block)
-    int32_t tb_flip;      // interior segments reverse their march every launch
     // reciprocals of dx, dy, dx*dx, dy*dy; sp_pow2 = 1 when all four spacings
     // are exact powers of two (then sdiv multiplies, bit-identically)
     float r_dx, r_dy, r_dxx, r_dyy;
@@ -294,7 +293,7 @@ constexpr int kMgMaxLevels = 40;
 void launch_sor_color(float *pp, const float *rhs, int nx, int ny, const SorConst &k, int color,
                       Ctl *ctl, uint32_t *err_slots, int pass, int it, int tol, float p_tol, int res,
                       hipStream_t s);
-// One whole red-black iteration per launch (k_sor_fused) over the local
+// One whole red-black iteration per launch (k_sor_march) over the local
 // interior rows [row_lo, row_hi) of a slab starting at global row j0 (p' and
 // rhs rows readable in [lo_clamp, hi_clamp]), ping-pong between pa / pb from
 // ctl->cur (iteration `it` reads buffer (cur + it) & 1; it = 0 reads nothing:
@@ -331,21 +330,9 @@ void launch_mg_final_residual(const MgLevel &L, const float *p, uint32_t *slots,
 void launch_corrector(const Geom &g, const Fields &f, int pass, float dt_override,
                       hipStream_t s);
 void launch_boundary(const Geom &g, const Fields &f, hipStream_t s);
-// fold_finalize: the finish launch also does launch_step_finalize's work
-// (its last workgroup; only where correct_finish_folds_finalize() says the
-// marching form runs, and only with no all-reduce between the two)
-bool correct_finish_folds_finalize(const Geom &g, const Fields &f);
-// A fixed-count solve's deferred k_finalize_solve (sf != null): the finish
-// launch's workgroup 0 does it (marching form; otherwise the finalize is
-// launched first), every workgroup reading p' from pp_new, the buffer the
-// flip makes current.  correct_finish_march(): the marching form runs.
-struct SolveFinalizeArgs {
-    const float *pp_new;
-    int pass, iters, check_break, flips;
-};
-bool correct_finish_march(const Geom &g, const Fields &f);
-void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
-                           bool fold_finalize = false, const SolveFinalizeArgs *sf = nullptr);
+// The corrector finish: the 16-row band march where the fields allow float4
+// access (nx % 4 == 0, 16-byte aligned arrays), else the scalar form.
+void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s);
 void launch_step_reduce(const Geom &g, const Fields &f, hipStream_t s);
 // The corrector of pass `pass` and, when pass+1 exists (has_next) and the
 // device's go flag says it runs, pass+1's head (u* <- u, v* <- v,

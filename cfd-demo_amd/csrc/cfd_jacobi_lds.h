@@ -733,8 +733,7 @@ __global__ __launch_bounds__(kLdsWaves * 64, lds_min_waves(MODE)) void k_jacobi_
 // s_sleep), then ONE agent acquire (buffer_inv sc1) + vmcnt(0) + the
 // workgroup barrier before any p' load.  The launch runs several workgroups
 // per CU, outside the table under which sc1 loads alone may replace the
-// acquire, so the acquire stays (acq = 1; CFD_PERSIST_ACQ=0 opts out for
-// measurement only).  Flags and claim counters hold epoch * 2^kPersistBlockBits
+// acquire, so the acquire stays (acq = 1).  Flags and claim counters hold epoch * 2^kPersistBlockBits
 // + blocks done / claimed (a solve has at most kMaxSweeps / 8 = 512 blocks);
 // the host gives every persistent launch a new epoch (never under graph
 // capture: arguments would freeze), so a value below the epoch's base reads
@@ -1071,14 +1070,7 @@ template <int T, int FAST, int MODE>
 int lds_segments(const Geom &g, int nrows, int nwc, int pad, int occ_override = 0) {
     if (g.tb_rows > 0) return cdiv(nrows, g.tb_rows);
     constexpr int kMaxRows = 160, kMinRows = 8;
-    // CFD_LDS_BPC caps the workgroups per CU a round is sized for (below the
-    // occupancy limit: fewer, longer segments, less warm-up recompute)
-    static const int bpc_cap = [] {
-        const char *e = getenv("CFD_LDS_BPC");
-        return e ? std::max(1, atoi(e)) : 0;
-    }();
-    const int occ = occ_override > 0 ? occ_override : lds_blocks_per_cu<T, FAST, MODE>(pad);
-    const int bpc = bpc_cap > 0 ? std::min(occ, bpc_cap) : occ;
+    const int bpc = occ_override > 0 ? occ_override : lds_blocks_per_cu<T, FAST, MODE>(pad);
     const int wgs_per_col = std::max(1, g.n_cu * bpc / nwc);
     const int per_round = kLdsWaves * wgs_per_col;
     // the persistent launch (occ_override) keeps ONE round whatever the
@@ -1197,9 +1189,7 @@ bool launch_lds_persist_t(const Geom &g, const Fields &f, int pass, int par0, in
     const int reach = T + 2;
     const int wlo = out_lo - reach <= 1 - g.j0 ? kEdgeWeight : 16;
     const int whi = out_hi + reach >= g.ny - 2 - g.j0 ? kEdgeWeight : 16;
-    // the agent acquire after each poll (CFD_PERSIST_ACQ=0: measurement only)
-    const char *ae = getenv("CFD_PERSIST_ACQ");
-    const int acq = ae ? (atoi(ae) != 0) : 1;
+    const int acq = 1;   // the agent acquire after each poll (MI355X_MICROARCH.md)
     // wait deadline in s_memrealtime ticks (100 MHz): CFD_PERSIST_DEADLINE_US,
     // default 10 s (a wait that long is a fault; time-sliced GPUs stay far
     // below it)

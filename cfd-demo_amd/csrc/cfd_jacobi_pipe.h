@@ -356,9 +356,7 @@ __global__ CFD_PIPE_BOUNDS void k_jacobi_pipe(
     // addition commutative, so the bits are the same): neighbouring segments
     // then read the rows they share at the same time, from L2, instead of one
     // at its start and the other at its end.
-    // With g.tb_flip the pattern also alternates per launch (par): a wave then
-    // starts on the rows it wrote last in the previous launch, still in L2.
-    if (!edge && ((seg + (g.tb_flip ? par : 0)) & 1)) {
+    if (!edge && (seg & 1)) {
         w.abase = r0 + r1 - 1;
         w.dir = -1;
     }

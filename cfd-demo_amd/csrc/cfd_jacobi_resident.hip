@@ -63,7 +63,7 @@ constexpr int kResMaxT = 8;
 template <int FAST, int WAVES, int ROWS>
 __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
     Geom g, Fields f, int pass, int iters, int T, int BR, int BC, int tiles_x, int ntiles,
-    int res_hi, uint32_t deadline, int late, int fin, int check_break, int xbar) {
+    int res_hi, uint32_t deadline, int late, int fin, int check_break) {
     constexpr int kResWaves = WAVES;
     extern __shared__ float lds_dyn[];
     __shared__ float red_s[kResWaves][kResMaxT];
@@ -279,12 +279,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
                     __builtin_amdgcn_s_sleep(1);
                 }
             };
-            if (!xbar) {
-                // one counter, G pollers
-                __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wait_ge(bar, (uint32_t)G * (uint32_t)(k + 1));
-            } else {
-                // two levels (MI355X_MICROARCH.md barrier-xcd): workgroup w
+            {
+                // two levels (MI355X_MICROARCH.md barrier-xcd; one counter with
+                // G pollers measured 3.99 vs 3.59 ms per step, r4): workgroup w
                 // arrives on group counter w % 8 (round-robin dispatch puts a
                 // group on one XCD: speed only, never correctness); the
                 // group's last arriver (told by its returning add) arrives on
@@ -370,63 +367,39 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
 struct ResidentPlan {
     int BR, BC, tiles_x, ntiles, G, lds;
 };
-// CFD_RESIDENT_TILE=<rows>x<cols> forces the tile shape (measurement)
 
 inline int resident_lds_bytes(int BR, int BC, int T) { return 3 * (BR + 2 * T) * (BC + 2 * T) * 4; }
 
-// 8 waves (512 threads) by default: the occupancy query admits two per CU
-// (the residency rule above); CFD_RESIDENT_WAVES=16 asks for 1,024-thread
-// workgroups, taken only where two of those fit a CU as well
-inline int resident_waves() {
-    const char *e = getenv("CFD_RESIDENT_WAVES");
-    return e && atoi(e) == 16 ? 16 : 8;
-}
+// The launched instantiation: 8 waves (512 threads; the occupancy query admits
+// two per CU, the residency rule above) and one row per thread step (r6: the
+// reference default 3.60 -> 3.23 ms per step at 18 x 48 tiles against 3.33
+// with 2 rows; 16-wave workgroups -1.5 %, not taken: profiles/r6/prof_r6j,
+// prof_r6m).
+constexpr int kResLaunchWaves = 8, kResLaunchRows = 1;
 
-// rows per thread step: 1 by default since r6 (with the r6 tile candidates:
-// the reference default 3.60 -> 3.23 ms per step at 18 x 48 tiles, against
-// 3.33 with 2 rows, profiles/r6/prof_r6j/ab_refdef3.log); CFD_RESIDENT_ROWS=2 / 4
-inline int resident_rows() {
-    const char *re = getenv("CFD_RESIDENT_ROWS");
-    const int r = re ? atoi(re) : 1;
-    return r == 2 || r == 4 ? r : 1;
-}
-
-// Workgroups of the instantiation that will be launched (waves, rows per
-// thread) per CU with `lds` bytes of dynamic LDS; cached per (instantiation,
-// lds) -- the plan is consulted on every tolerance-mode solve
+// Workgroups of the launched instantiation per CU with `lds` bytes of dynamic
+// LDS; cached per lds -- the plan is consulted on every tolerance-mode solve
 template <int FAST>
 int resident_blocks_per_cu(int lds) {
     static std::mutex mu;
-    static std::map<std::pair<int, int>, int> cache;
-    const int waves = resident_waves(), rows = resident_rows();
-    const int key = waves * 16 + rows;
+    static std::map<int, int> cache;
     std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find({key, lds});
+    auto it = cache.find(lds);
     if (it != cache.end()) return it->second;
-    const void *k = waves == 16 ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 16, 2>)
-                    : rows == 1 ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 1>)
-                    : rows == 4 ? reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 4>)
-                                : reinterpret_cast<const void *>(&k_jacobi_resident<FAST, 8, 2>);
+    const void *k =
+        reinterpret_cast<const void *>(&k_jacobi_resident<FAST, kResLaunchWaves, kResLaunchRows>);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, waves * 64, lds) != hipSuccess) n = 0;
-    cache[{key, lds}] = n;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kResLaunchWaves * 64, lds) != hipSuccess)
+        n = 0;
+    cache[lds] = n;
     return n;
-}
-
-// workgroups per CU the grid may use (CFD_RESIDENT_GPC, 1 or 2): 2 spreads
-// smaller tiles over twice the workgroups (two per CU, so every grid-barrier
-// wait has a second workgroup to hide behind); the launch is then taken only
-// where the occupancy query admits 3 per CU (a margin over the 2 it needs)
-inline int resident_gpc() {
-    const char *e = getenv("CFD_RESIDENT_GPC");
-    return e && atoi(e) == 2 ? 2 : 1;
 }
 
 // Tile shape: the candidate with the least LDS-box work per workgroup
 // (ceil(tiles / G) x box cells), every candidate admitting 2 workgroups per CU
-// (gpc 1; 3 with gpc 2).  Single domain only (rows 0..ny-1 owned; the fields'
-// ghost rows unused).  The occupancy queries are cached; the rest is a few
-// integer operations.
+// (one per CU in the grid, a margin of one).  Single domain only (rows
+// 0..ny-1 owned; the fields' ghost rows unused).  The occupancy queries are
+// cached; the rest is a few integer operations.
 bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
     if (g.nx < 4 || g.ny < 4 || g.j0 != 0 || g.nyl != g.ny) return false;
     // box widths BC + 2e (e = 0..T-1) fill 64-lane passes: BC = 48 -> 48..62
@@ -436,23 +409,18 @@ bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
     // (profiles/r6/prof_r6i, prof_r6j)
     static const int cand[][2] = {{8, 48},  {16, 48},  {18, 48},  {20, 48},
                                   {24, 48}, {32, 48},  {16, 112}, {32, 112}};
-    const int gpc = resident_gpc();
     long best = -1;
     for (const auto &cd : cand) {
-        int BR = cd[0], BC = cd[1];
-        if (const char *te = getenv("CFD_RESIDENT_TILE")) {
-            if (sscanf(te, "%dx%d", &BR, &BC) != 2 || BR < 2 || BC < 2) return false;
-            if (&cd != &cand[0]) break;
-        }
+        const int BR = cd[0], BC = cd[1];
         const int lds = resident_lds_bytes(BR, BC, T);
         const int occ = g.res_div == 1   ? resident_blocks_per_cu<1>(lds)
                         : g.res_div == 2 ? resident_blocks_per_cu<2>(lds)
                         : g.res_div == 3 ? resident_blocks_per_cu<3>(lds)
                                          : resident_blocks_per_cu<0>(lds);
-        if (occ < gpc + 1) continue;
+        if (occ < 2) continue;
         const int tx = cdiv(g.nx, BC), ty = cdiv(g.ny, BR);
         const long nt = (long)tx * ty;
-        const int G = (int)std::min<long>(nt, (long)gpc * g.n_cu);
+        const int G = (int)std::min<long>(nt, (long)g.n_cu);
         const long work = (long)cdiv(nt, G) * (BR + 2 * T) * (BC + 2 * T);
         if (best < 0 || work < best) {
             best = work;
@@ -471,16 +439,10 @@ static int resident_simd_end(int nx) {
     return e;
 }
 
-// sweeps per block between barriers (CFD_RESIDENT_T, 2..8; default 8)
-static int resident_T() {
-    const char *e = getenv("CFD_RESIDENT_T");
-    return e ? std::max(2, std::min(kResMaxT, atoi(e))) : kResMaxT;
-}
-
 bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters, int fin,
                             int check_break, hipStream_t s) {
     if (iters <= 0) return false;
-    const int T = resident_T();
+    constexpr int T = kResMaxT;   // sweeps per block between grid barriers
     ResidentPlan p;
     if (!resident_plan(g, T, &p)) return false;
     const char *de = getenv("CFD_PERSIST_DEADLINE_US");
@@ -488,33 +450,18 @@ bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters,
     const uint32_t deadline = (uint32_t)std::min(4.0e9, dl_us * 100.0);
     const char *le = getenv("CFD_PERSIST_LATE");
     const int late = le ? std::max(0, atoi(le)) : 0;
-    // the grid barrier: two-level (default) or one counter (CFD_RESIDENT_BAR=flat)
-    const char *be = getenv("CFD_RESIDENT_BAR");
-    const int xbar = be && strcmp(be, "flat") == 0 ? 0 : 1;
-    const int rows = resident_rows();
-#define CFD_RES_LAUNCH(FASTV, WV, RW)                                                              \
-    hipLaunchKernelGGL((k_jacobi_resident<FASTV, WV, RW>), dim3(p.G), dim3(WV * 64), p.lds, s, g, \
-                       f, pass, iters, T, p.BR, p.BC, p.tiles_x, p.ntiles,                        \
-                       resident_simd_end(g.nx), deadline, late, fin, check_break, xbar)
-#define CFD_RES_WAVES(FASTV)                \
-    if (resident_waves() == 16)             \
-        CFD_RES_LAUNCH(FASTV, 16, 2);       \
-    else if (rows == 1)                     \
-        CFD_RES_LAUNCH(FASTV, 8, 1);        \
-    else if (rows == 4)                     \
-        CFD_RES_LAUNCH(FASTV, 8, 4);        \
-    else                                    \
-        CFD_RES_LAUNCH(FASTV, 8, 2);
-    if (g.res_div == 1) {
-        CFD_RES_WAVES(1)
-    } else if (g.res_div == 2) {
-        CFD_RES_WAVES(2)
-    } else if (g.res_div == 3) {
-        CFD_RES_WAVES(3)
-    } else {
-        CFD_RES_WAVES(0)
-    }
-#undef CFD_RES_WAVES
+#define CFD_RES_LAUNCH(FASTV)                                                                       \
+    hipLaunchKernelGGL((k_jacobi_resident<FASTV, kResLaunchWaves, kResLaunchRows>), dim3(p.G),      \
+                       dim3(kResLaunchWaves * 64), p.lds, s, g, f, pass, iters, T, p.BR, p.BC,     \
+                       p.tiles_x, p.ntiles, resident_simd_end(g.nx), deadline, late, fin, check_break)
+    if (g.res_div == 1)
+        CFD_RES_LAUNCH(1);
+    else if (g.res_div == 2)
+        CFD_RES_LAUNCH(2);
+    else if (g.res_div == 3)
+        CFD_RES_LAUNCH(3);
+    else
+        CFD_RES_LAUNCH(0);
 #undef CFD_RES_LAUNCH
     return true;
 }
@@ -522,7 +469,7 @@ bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters,
 bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *wgs) {
     // (the tile plan the launch would take; false: none fits)
     ResidentPlan p;
-    if (!resident_plan(g, resident_T(), &p)) return false;
+    if (!resident_plan(g, kResMaxT, &p)) return false;
     *br = p.BR;
     *bc = p.BC;
     *tiles = p.ntiles;

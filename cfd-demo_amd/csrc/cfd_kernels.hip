@@ -129,100 +129,17 @@ __global__ __launch_bounds__(kBlock) void k_predict(Geom g, Fields f, float dt_o
         f.v_star[(long)lj * g.nx + i] = v_pred_val<SCHEME, SP>(g, f, dt_of(f.ctl, dt_override), i, lj, a);
 }
 
-// Register-backed stencil for k_predict4: u rows lj-1..lj+1 and v rows
-// lj-1..lj+1 at columns i0-1..i0+4, column q of the thread's four.  Every
-// (di, dj) the first-order helpers ask for is a compile-time index once the
-// column loop is unrolled, so the values never leave registers.
-struct RAcc {
-    const float (&ur)[3][6];
-    const float (&vr)[3][6];
-    int q;
-    __device__ __forceinline__ float U(int di, int dj) const { return ur[dj + 1][q + 1 + di]; }
-    __device__ __forceinline__ float V(int di, int dj) const { return vr[dj + 1][q + 1 + di]; }
-};
-
 // Both first-order predictors with four columns per thread (i0 = 4t): the
 // pitch-nx v rows move as float4 (v row lj-1, lj, lj+1 and the v* store), the
 // pitch-(nx+1) u rows as scalars, and each value is loaded once for the eight
-// faces it feeds (u_pred_val / v_pred_val over an RAcc, so the arithmetic is
+// faces it feeds (u_pred_val / v_pred_val over an RAccN, so the arithmetic is
 // the single-face kernel's, bit for bit).  Face 0 and column 0 are not
 // predicted (model.rs:538, :586); the thread owning columns nx-4..nx-1 also
 // predicts u face nx, through the flat-indexed GAcc (its east and north
 // neighbours wrap to the next row, Q1-Q3).  Requires 16-byte aligned v and
 // v* rows (checked by the launcher).
-template <int SP>
-__global__ __launch_bounds__(kBlock) void k_predict4(Geom g, Fields f, float dt_override,
-                                                     int row_lo, int u_hi, int v_hi, int nbx) {
-    const int bid = xcd_block(g);
-    const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
-    const int lj = row_lo + bid / nbx;
-    const int nx = g.nx, W = nx + 1;
-    if (i0 >= nx) return;
-    const float dtv = dt_of(f.ctl, dt_override);   // once: a per-face reload waits on every load
-    const float *__restrict__ u = f.u;
-    const float *__restrict__ v = f.v;
-    const long ku = (long)lj * W + i0, kv = (long)lj * nx + i0;
-    const bool do_u = lj <= u_hi, do_v = lj <= v_hi;
-    float ur[3][6], vr[3][6];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) ur[r][c] = vr[r][c] = 0.0f;
-    // shared by both predictors: u row lj (cols i0-1..i0+4), v rows lj, lj+1
-    ur[1][0] = i0 > 0 ? u[ku - 1] : 0.0f;
-#pragma unroll
-    for (int c = 0; c < 5; ++c) ur[1][c + 1] = u[ku + c];
-    {
-        const float4 a = *reinterpret_cast<const float4 *>(v + kv);
-        const float4 b = *reinterpret_cast<const float4 *>(v + kv + nx);
-        vr[1][1] = a.x; vr[1][2] = a.y; vr[1][3] = a.z; vr[1][4] = a.w;
-        vr[2][1] = b.x; vr[2][2] = b.y; vr[2][3] = b.z; vr[2][4] = b.w;
-    }
-    if (do_u) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            ur[0][c + 1] = u[ku - W + c];
-            ur[2][c + 1] = u[ku + W + c];
-        }
-    }
-    if (do_v) {
-        const float4 a = *reinterpret_cast<const float4 *>(v + kv - nx);
-        vr[0][1] = a.x; vr[0][2] = a.y; vr[0][3] = a.z; vr[0][4] = a.w;
-        vr[1][0] = i0 > 0 ? v[kv - 1] : 0.0f;
-        vr[1][5] = v[kv + 4];   // column nx wraps to the next row's column 0 (flat index)
-    }
-    if (do_u) {
-        float o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            o[q] = u_pred_val<0, SP>(g, f, dtv, i0 + q, lj, RAcc{ur, vr, q});
-        float *__restrict__ us = f.u_star + ku;
-        if (i0 > 0) us[0] = o[0];
-        us[1] = o[1];
-        us[2] = o[2];
-        us[3] = o[3];
-        if (i0 + 4 == nx) {
-            const GAcc a{f.u, f.v, ku + 4, kv + 4, W, nx};
-            us[4] = u_pred_val<0, SP>(g, f, dtv, nx, lj, a);
-        }
-    }
-    if (do_v) {
-        float o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            o[q] = v_pred_val<0, SP>(g, f, dtv, i0 + q, lj, RAcc{ur, vr, q});
-        float *__restrict__ vs = f.v_star + kv;
-        if (i0 > 0) {
-            *reinterpret_cast<float4 *>(vs) = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
-            vs[1] = o[1];
-            vs[2] = o[2];
-            vs[3] = o[3];
-        }
-    }
-}
-
-// k_predict4 over RPT consecutive rows per thread: the window of u and v rows
+// Each thread takes RPT = 2 consecutive rows (96 vs 104 us for one row and
+// 107 for four, r1): the window of u and v rows
 // lj-1 .. lj+RPT is loaded up front (every load in flight at once, and the
 // rows shared by neighbouring output rows loaded once), then the 8 x RPT
 // faces are computed with the same u_pred_val / v_pred_val arithmetic.
@@ -1189,18 +1106,10 @@ __device__ __forceinline__ float cf_u_face(const Geom &g, float inlet, float dt,
 // Same values and maxima as k_correct_finish (one float per thread held the
 // kernel near 4.7 TB/s, like the divergence before it went to float4).
 // Requires 16-byte aligned p', p, v*, v (checked by the launcher).
-// k_step_finalize's work (model.rs:333-377, :877-889) for one workgroup.
-// COHERENT: run by the last workgroup of the launch that published the step
-// maxima (k_correct_finish4m's fold): the maxima and the non-finite flag were
-// written by other workgroups' atomics, so they are read with device-scope
-// atomic loads (from L2, never a stale per-CU cache line).
-template <bool COHERENT>
-__device__ __forceinline__ uint32_t ld_ctl_t(const uint32_t *p) {
-    return COHERENT ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
-}
-template <bool COHERENT>
+// k_step_finalize's work (model.rs:333-377, :877-889) for one workgroup (its
+// own launch: the maxima the previous launches published are visible).
 __device__ __forceinline__ void step_finalize_body(const Geom &g, const Fields &f) {
-    auto ld_ctl = [](const uint32_t *p) { return ld_ctl_t<COHERENT>(p); };
+    auto ld_ctl = [](const uint32_t *p) { return *p; };
     Ctl *c = f.ctl;
     if (threadIdx.x < 4) {   // fold the spread step maxima (sharded: already folded)
         uint32_t *set = f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride;
@@ -1259,15 +1168,15 @@ __global__ void k_abort_to_red(Fields f) {
 // (k_step_finalize's part of it, for the entry points with no step finalize:
 // cfd_piso_step, cfd_pressure_solve).
 __global__ void k_abort_from_red(Fields f) {
-    if (threadIdx.x != 0 || !ld_ctl_t<false>(&f.ctl->red[6])) return;
+    if (threadIdx.x != 0 || !f.ctl->red[6]) return;
     if (f.persist) __hip_atomic_store(f.persist + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (f.host_nonfinite)
         __hip_atomic_store(f.host_nonfinite + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void k_step_finalize(Geom g, Fields f) { step_finalize_body<false>(g, f); }
+__global__ void k_step_finalize(Geom g, Fields f) { step_finalize_body(g, f); }
 
-// One row of k_correct_finish4's work for the 4 columns i0..i0+3 of local
+// One row of k_correct_finish4m's work for the 4 columns i0..i0+3 of local
 // row lj: pc = p' row lj, pb = p' row lj-1 (loaded by the caller), the step
 // maxima and the non-finite flag accumulate into du..bad.
 template <int SP>
@@ -1343,72 +1252,16 @@ __device__ __forceinline__ void cf4_row(const Geom &g, const Fields &f, const fl
     }
 }
 
-template <int SP>
-__global__ __launch_bounds__(kBlock) void k_correct_finish4(Geom g, Fields f, float dt_override,
-                                                            int nbx) {
-    Ctl *c = f.ctl;
-    const int nx = g.nx;
-    float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
-    bool bad = false;
-    const long ntiles = (long)nbx * (g.nyl + 1);
-    const int bid = xcd_block(g), G = (int)gridDim.x;
-    const long t_lo = ntiles * bid / G, t_hi = ntiles * (bid + 1) / G;
-    const float dt = dt_of(c, dt_override);
-    const float inlet = c->inlet;
-    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
-    for (long t = t_lo; t < t_hi; ++t) {
-        const int i0 = 4 * ((int)(t % nbx) * kBlock + (int)threadIdx.x);
-        const int lj = (int)(t / nbx);
-        if (i0 >= nx) continue;
-        const int j = g.j0 + lj;
-        const long rp = (long)lj * nx + i0;
-        const bool vrow = (j != 0 && j != g.ny);
-        float4 pc = make_float4(0.f, 0.f, 0.f, 0.f), pb = pc;
-        if (lj < g.nyl || vrow) pc = *reinterpret_cast<const float4 *>(pp + rp);
-        if (vrow) pb = *reinterpret_cast<const float4 *>(pp + rp - nx);
-        cf4_row<SP>(g, f, pp, inlet, dt, i0, lj, pc, pb, du, dv, mu, mv, bad);
-    }
-    flag_nonfinite(c, bad);
-    __shared__ float red[kBlock / 64][4];
-    du = wave_max(du);
-    dv = wave_max(dv);
-    mu = wave_max(mu);
-    mv = wave_max(mv);
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        red[wv][0] = du;
-        red[wv][1] = dv;
-        red[wv][2] = mu;
-        red[wv][3] = mv;
-    }
-    __syncthreads();
-    if (threadIdx.x < 4) {
-        float r = 0.f;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) r = fmaxf(r, red[w][threadIdx.x]);
-        publish_max(f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride, bid, r);
-    }
-}
-
-// k_correct_finish4 with a thread marching down a band of kCfRows rows of its
-// 4 columns: p' row lj, loaded for row lj, is row lj+1's lower neighbour (the
-// v correction's p'(j-1)), so every p' row crosses HBM once instead of twice.
-// FIN: the launch's last workgroup also does k_step_finalize's work (an
-// unsharded step has no all-reduce between the two): one launch less per step.
+// The corrector finish (model.rs:825-850's corrections, the boundary rows and
+// the step maxima) for 4 columns per thread, each thread marching down a band
+// of kCfRows rows: p' row lj, loaded for row lj, is row lj+1's lower neighbour
+// (the v correction's p'(j-1)), so every p' row crosses HBM once instead of
+// twice.
 constexpr int kCfRows = 16;
-// FS: workgroup 0 first does the solve's k_finalize_solve work (fixed-count
-// solve: the flip count is the host's), so that launch goes; every workgroup
-// takes p' from pp_new (the buffer the flip makes current) instead of
-// reading Ctl::cur, which workgroup 0 rewrites.
-struct FinDefer {
-    const float *pp_new;
-    int pass, iters, check_break, flips;
-};
-template <int SP, bool FIN, bool FS>
+template <int SP>
 __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, float dt_override,
-                                                             int nbx, FinDefer fd) {
+                                                             int nbx) {
     Ctl *c = f.ctl;
-    if (FS && blockIdx.x == 0) solve_finalize_body(g, f, fd.pass, fd.iters, fd.check_break, fd.flips, 0);
     const int nx = g.nx;
     float du = 0.f, dv = 0.f, mu = 0.f, mv = 0.f;
     bool bad = false;
@@ -1417,7 +1270,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, f
     const int l0 = (bid / nbx) * kCfRows, l1 = min(l0 + kCfRows, g.nyl + 1);
     const float dt = dt_of(c, dt_override);
     const float inlet = c->inlet;
-    const float *__restrict__ pp = FS ? fd.pp_new : (c->cur ? f.pp[1] : f.pp[0]);
+    const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
     if (i0 < nx) {
         float4 pb = make_float4(0.f, 0.f, 0.f, 0.f);
         {
@@ -1454,17 +1307,6 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, f
         for (int w = 0; w < kBlock / 64; ++w) r = fmaxf(r, red[w][threadIdx.x]);
         publish_max(f.red_slots + (size_t)threadIdx.x * kResSlots * kResStride, bid, r);
     }
-    if (!FIN) return;
-    // last workgroup to finish: every other one's maxima and flag are out
-    __shared__ unsigned ticket;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) ticket = atomicAdd(&c->done, 1u);
-    __syncthreads();
-    if (ticket != gridDim.x - 1) return;
-    __threadfence();
-    step_finalize_body<true>(g, f);
-    if (threadIdx.x == 0) c->done = 0u;
 }
 
 // ------------------------------------------------- step reductions (K7)
@@ -1573,29 +1415,12 @@ void launch_predict(const Geom &g, const Fields &f, float dt_override, hipStream
     auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
     if (vec && g.scheme == 0 && g.nx % 4 == 0 && a16(f.v) && a16(f.v_star)) {
         const int nbx4 = cdiv(g.nx / 4, kBlock);
-        static const int rpt = [] {
-            // 2 rows per thread: 96 vs 104 (1 row) and 107 us (4 rows), r1 tb_one
-            const char *e = getenv("CFD_PRED_RPT");
-            return e ? atoi(e) : 2;
-        }();
-        if (rpt == 2 || rpt == 4) {
-            const dim3 gr(nbx4 * cdiv(ghi - glo + 1, rpt));
-#define CFD_LAUNCH_PR(SPV, R) hipLaunchKernelGGL((k_predict4r<SPV, R>), gr, dim3(kBlock), 0, s, g, f, \
-                                                 dt_override, glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx4)
-            if (rpt == 2) {
-                if (g.sp_pow2) CFD_LAUNCH_PR(1, 2); else CFD_LAUNCH_PR(0, 2);
-            } else {
-                if (g.sp_pow2) CFD_LAUNCH_PR(1, 4); else CFD_LAUNCH_PR(0, 4);
-            }
-#undef CFD_LAUNCH_PR
-            return;
-        }
-        const dim3 grid4(nbx4 * (ghi - glo + 1));
+        const dim3 gr(nbx4 * cdiv(ghi - glo + 1, 2));
         if (g.sp_pow2)
-            hipLaunchKernelGGL(k_predict4<1>, grid4, dim3(kBlock), 0, s, g, f, dt_override,
+            hipLaunchKernelGGL((k_predict4r<1, 2>), gr, dim3(kBlock), 0, s, g, f, dt_override,
                                glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx4);
         else
-            hipLaunchKernelGGL(k_predict4<0>, grid4, dim3(kBlock), 0, s, g, f, dt_override,
+            hipLaunchKernelGGL((k_predict4r<0, 2>), gr, dim3(kBlock), 0, s, g, f, dt_override,
                                glo - g.j0, u_hi - g.j0, v_hi - g.j0, nbx4);
         return;
     }
@@ -1621,21 +1446,14 @@ void launch_predict_div(const Geom &g, const Fields &f, float dt_override, hipSt
     const int glo = (g.j0 > 1 ? g.j0 : 1) - g.j0;
     const int u_hi = ((g.j0 + g.nyl - 1) < (g.ny - 2) ? (g.j0 + g.nyl - 1) : (g.ny - 2)) - g.j0;
     const int v_hi = ((g.j0 + g.nyl) < (g.ny - 1) ? (g.j0 + g.nyl) : (g.ny - 1)) - g.j0;
-    static const int rpt = [] {
-        const char *e = getenv("CFD_PRED_DIV_RPT");
-        return e && atoi(e) == 4 ? 4 : 2;
-    }();
+    constexpr int rpt = 2;   // rows per thread
     const int nwc = cdiv(g.nx / 4, 63);
     const int ntile = cdiv(g.nyl, rpt);
     const dim3 grid(nwc * cdiv(ntile, kBlock / 64));
 #define CFD_LAUNCH_PD(SPV, R)                                                                    \
     hipLaunchKernelGGL((k_predict_div<SPV, R>), grid, dim3(kBlock), 0, s, g, f, dt_override, glo, \
                        u_hi, v_hi, nwc, ntile)
-    if (rpt == 4) {
-        if (g.sp_pow2) CFD_LAUNCH_PD(1, 4); else CFD_LAUNCH_PD(0, 4);
-    } else {
-        if (g.sp_pow2) CFD_LAUNCH_PD(1, 2); else CFD_LAUNCH_PD(0, 2);
-    }
+    if (g.sp_pow2) CFD_LAUNCH_PD(1, 2); else CFD_LAUNCH_PD(0, 2);
 #undef CFD_LAUNCH_PD
 }
 
@@ -1786,69 +1604,15 @@ void launch_correct_head(const Geom &g, const Fields &f, int pass, float dt_over
 #undef CFD_LAUNCH_CH
 }
 
-bool correct_finish_folds_finalize(const Geom &g, const Fields &f) {
+void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s) {
     auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-    const char *v = getenv("CFD_CF_VEC"), *m = getenv("CFD_CF_MARCH"), *fz = getenv("CFD_CF_FOLD");
-    // opt-in (CFD_CF_FOLD=1): the device-scope release fence every workgroup
-    // needs before its ticket writes its XCD's L2 back (buffer_wbl2; the 8
-    // XCDs have separate L2s), which cost the step 90 us against the ~8 us
-    // launch it saves (r2: 1.318 vs 1.226 ms per step)
-    return fz && atoi(fz) == 1 && !(v && atoi(v) == 0) && !(m && atoi(m) == 0) &&
-           g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star);
-}
-
-bool correct_finish_march(const Geom &g, const Fields &f) {
-    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-    const char *v = getenv("CFD_CF_VEC"), *m = getenv("CFD_CF_MARCH");
-    return !(v && atoi(v) == 0) && !(m && atoi(m) == 0) && g.nx % 4 == 0 && a16(f.pp[0]) &&
-           a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star);
-}
-
-void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hipStream_t s,
-                           bool fold_finalize, const SolveFinalizeArgs *sf) {
-    static const int vec = [] {
-        const char *e = getenv("CFD_CF_VEC");
-        return e ? atoi(e) : 1;
-    }();
-    auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-    if (vec && g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) &&
-        a16(f.v_star)) {
+    if (g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star)) {
         const int nbx = cdiv(g.nx / 4, kBlock);
-        static const bool march = [] {
-            const char *e = getenv("CFD_CF_MARCH");
-            return !(e && atoi(e) == 0);
-        }();
-        if (march) {
-            const dim3 grid(nbx * cdiv(g.nyl + 1, kCfRows));
-            FinDefer fd{};
-            if (sf) fd = FinDefer{sf->pp_new, sf->pass, sf->iters, sf->check_break, sf->flips};
-#define CFD_LAUNCH_CF4M(SPV, FINV, FSV)                                                          \
-            hipLaunchKernelGGL((k_correct_finish4m<SPV, FINV, FSV>), grid, dim3(kBlock), 0, s, g, f, \
-                               dt_override, nbx, fd)
-#define CFD_LAUNCH_CF4M2(SPV, FINV) \
-            if (sf) { CFD_LAUNCH_CF4M(SPV, FINV, true); } else { CFD_LAUNCH_CF4M(SPV, FINV, false); }
-            if (g.sp_pow2 && fold_finalize) {
-                CFD_LAUNCH_CF4M2(1, true);
-            } else if (g.sp_pow2) {
-                CFD_LAUNCH_CF4M2(1, false);
-            } else if (fold_finalize) {
-                CFD_LAUNCH_CF4M2(0, true);
-            } else {
-                CFD_LAUNCH_CF4M2(0, false);
-            }
-#undef CFD_LAUNCH_CF4M2
-#undef CFD_LAUNCH_CF4M
-            return;
-        }
-        if (sf) launch_finalize_solve(g, f, sf->pass, sf->iters, sf->check_break, sf->flips, s);
-        const long ntiles = (long)nbx * (g.nyl + 1);
-        const int blocks = (int)std::min<long>(ntiles, 8L * g.n_cu);
+        const dim3 grid(nbx * cdiv(g.nyl + 1, kCfRows));
         if (g.sp_pow2)
-            hipLaunchKernelGGL(k_correct_finish4<1>, dim3(blocks), dim3(kBlock), 0, s, g, f,
-                               dt_override, nbx);
+            hipLaunchKernelGGL(k_correct_finish4m<1>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
         else
-            hipLaunchKernelGGL(k_correct_finish4<0>, dim3(blocks), dim3(kBlock), 0, s, g, f,
-                               dt_override, nbx);
+            hipLaunchKernelGGL(k_correct_finish4m<0>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
         return;
     }
     const int nbx = cdiv(g.nx + 1, kBlock);

@@ -119,7 +119,7 @@ struct cfd_model {
     // on cstream while the interior runs on stream (SURVEY.md §8(e) overlap)
     hipStream_t cstream = nullptr;
     hipEvent_t ev_ov0 = nullptr, ev_ov1 = nullptr, ev_rhs = nullptr, ev_uv = nullptr;
-    bool overlap = true;   // CFD_OVERLAP=0 serialises them
+    static constexpr bool overlap = true;
     cfd_grid grid{};
     cfd_params params{};
     Geom g{};
@@ -148,7 +148,7 @@ struct cfd_model {
     ncclComm_t comm = nullptr;
     LocalHub *hub = nullptr;   // testing stand-in for comm
     int host_cur = 0;   // mirror of ctl->cur, valid when the tolerance is off
-    // SOR: one fused launch per red-black iteration (k_sor_fused) where it
+    // SOR: one fused launch per red-black iteration (k_sor_march) where it
     // applies; CFD_SOR_FUSED=0 keeps the two color passes in place
     bool sor_fused = [] {
         const char *e = getenv("CFD_SOR_FUSED");
@@ -474,7 +474,7 @@ struct cfd_model {
         return k;
     }
 
-    // SOR on a slab (k_sor_fused over the owned interior rows): each
+    // SOR on a slab (k_sor_march over the owned interior rows): each
     // iteration reads 2 p' ghost rows per side (the red rows just outside the
     // slab are recomputed from them) and 1 rhs ghost row, so the written
     // buffer's 2 boundary rows go to the neighbours after every iteration.
@@ -1211,10 +1211,7 @@ struct cfd_model {
                         int T, lo, hi, exch;
                         plan_block((int)j0, g.nyl, g.ny, 0, k, tmax, iters, &T, &lo, &hi, &exch);
                         if (T != 8) break;
-                        if (k + T >= iters) {
-                            if (persist_res_env) res_it = iters - 1;
-                            else break;
-                        }
+                        if (k + T >= iters) res_it = iters - 1;
                         k += T;
                         ++nblk;
                     }
@@ -1367,11 +1364,6 @@ struct cfd_model {
         }
         if (resident) {
             // k_jacobi_resident's last workgroup finalized the solve
-        } else if (defer_finalize) {
-            // the corrector finish's workgroup 0 does it (one launch less)
-            fin_deferred = SolveFinalizeArgs{f.pp[(host_cur + launches) & 1], pass, iters,
-                                             pass >= 1 ? 1 : 0, launches};
-            fin_pending = true;
         } else {
             launch_finalize_solve(g, f, pass, iters, pass >= 1 ? 1 : 0, launches, stream,
                                   spec ? 2 : 0);
@@ -1582,12 +1574,8 @@ struct cfd_model {
         return e ? atoi(e) : -1;
     }();
     bool persist_env = persist_req != 0;
-    // the solve's last (residual) block inside the persistent launch too;
-    // CFD_PERSIST_RES=0 launches it on its own
-    bool persist_res_env = [] {
-        const char *e = getenv("CFD_PERSIST_RES");
-        return !(e && atoi(e) == 0);
-    }();
+    // (the solve's last, residual-publishing block runs inside the persistent
+    // launch too)
     // slabs: the blocks between two p' exchanges as one persistent launch,
     // opt-in (CFD_PERSIST_SHARDED=1).  r5 same-geometry A/B (the rank slabs'
     // owned rows + 2 x 32 ghost rows, the 24 KiB pad they get; medians of 3,
@@ -1693,25 +1681,16 @@ struct cfd_model {
         };
         if (finish) {
             first_divergence(host_driven() ? -1 : 0);
-            // a fixed-count Jacobi solve (its flip count is the host's) hands
-            // its finalize to the corrector finish's first workgroup
-            defer_finalize = !host_driven() && !g.tol_enabled &&
-                             params.pressure_solver == CFD_SOLVER_JACOBI && correct_finish_march(g, f) &&
-                             defer_finalize_env;
-            fin_pending = false;
             // a fixed-count step on slabs needs the solve's residual only for
             // reporting: it rides the step-end all-reduce (Ctl::red[5]) instead
             // of an all-reduce of its own
             merge_res_allreduce = sharded() && !host_driven();
             int rc = host_driven() ? enqueue_solve_host_driven(nullptr) : enqueue_solve(0);
             merge_res_allreduce = false;
-            defer_finalize = false;
             if (rc) return rc;
             phase_mark(1, false);
-            launch_correct_finish(g, f, dt_override, stream, step_finalize_folded,
-                                  fin_pending ? &fin_deferred : nullptr);
+            launch_correct_finish(g, f, dt_override, stream);
             phase_mark(1, true);
-            fin_pending = false;
             HIP_TRY(hipGetLastError());
             return 0;
         }
@@ -1765,28 +1744,16 @@ struct cfd_model {
     // rec_step: record the step's GPU time for cfd_get_residuals (the last
     // step of a cfd_update_n batch only: every event record on the stream
     // costs the step a few microseconds of dispatch)
-    bool step_begin_folded = false, step_finalize_folded = false;   // this step's (enqueue_update)
-    // the step's solve finalize handed to the corrector finish (enqueue_piso)
-    bool defer_finalize = false, fin_pending = false, merge_res_allreduce = false;
+    bool step_begin_folded = false;   // this step's (enqueue_update)
+    // fixed-count steps on slabs: the solve residual rides the step all-reduce
+    bool merge_res_allreduce = false;
     bool uv_async = false;   // this step's u/v exchange runs on cstream (enqueue_update)
-    SolveFinalizeArgs fin_deferred{};
-    // opt-in (CFD_SOLVE_FIN_FOLD=1): one launch less, but workgroup 0's extra
-    // serial work lengthens the finish by as much (r2: 1.2347/1.2298 vs
-    // 1.2342/1.2358 ms per step, tools/fin_ab.sh)
-    bool defer_finalize_env = [] {
-        const char *e = getenv("CFD_SOLVE_FIN_FOLD");
-        return e && atoi(e) == 1;
-    }();
     int enqueue_update(bool rec_step = true) {
         if (rec_step) HIP_TRY(hipEventRecord(ev_step0, stream));
         const bool fused = params.corrector_passes == 0;
-        // one launch less each side of the step where the fused kernels can
-        // carry the work: the predictor march sets the inlet ramp (all
-        // k_step_begin does when nothing is copied), and the corrector finish's
-        // last workgroup does k_step_finalize's (unsharded: no all-reduce
-        // between the two)
+        // one launch less where the predictor march can carry the work: it
+        // sets the inlet ramp (all k_step_begin does when nothing is copied)
         step_begin_folded = fused && predict_march_ok(g, f);
-        step_finalize_folded = fused && !sharded() && correct_finish_folds_finalize(g, f);
         if (!step_begin_folded) launch_step_begin(g, f, fused ? 0 : 1, stream);
         // slabs: the u/v ghost exchange runs on cstream while the predictor
         // march forms the rows that read no ghost (enqueue_piso)
@@ -1811,7 +1778,7 @@ struct cfd_model {
         if (sharded() && persist_env && persist_sharded_env) launch_abort_to_red(f, stream);
         rc = allreduce_max_u32(f.ctl->red, 7);   // maxima, non-finite flag, solve residual, abort
         if (rc) return rc;
-        if (!step_finalize_folded) launch_step_finalize(g, f, stream);
+        launch_step_finalize(g, f, stream);
         HIP_TRY(hipGetLastError());
         if (rec_step) HIP_TRY(hipEventRecord(ev_step1, stream));
         if (timing) timed_steps++;
@@ -2013,7 +1980,6 @@ struct cfd_model {
         *(volatile uint32_t *)h_nonfinite = 0u;
         host_cur = ck_host_cur;
         pp_ghosts_shallow = ck_shallow;
-        fin_pending = false;
         ++recoveries;
         std::vector<std::function<int()>> replay;
         replay.swap(ck_replay);
@@ -2199,7 +2165,6 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     HIP_TRY(hipEventCreateWithFlags(&m->ev_ov1, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&m->ev_rhs, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&m->ev_uv, hipEventDisableTiming));
-    if (const char *ov = getenv("CFD_OVERLAP")) m->overlap = atoi(ov) != 0;
     HIP_TRY(hipEventCreate(&m->ev_step0));
     HIP_TRY(hipEventCreate(&m->ev_step1));
     HIP_TRY(hipEventCreate(&m->ev_prof0));
@@ -2291,8 +2256,6 @@ int build_model(cfd_model *m, const cfd_grid *grid, const cfd_params *p, int dev
     }
     g.xcd_remap = 1;
     if (const char *xv = getenv("CFD_XCD_REMAP")) g.xcd_remap = atoi(xv) ? 1 : 0;
-    g.tb_flip = 0;
-    if (const char *fv = getenv("CFD_TB_FLIP")) g.tb_flip = atoi(fv) ? 1 : 0;
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||

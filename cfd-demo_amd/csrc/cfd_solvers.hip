@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
 // lanes x one column pair (one red and one black cell per row) and a segment
 // of R interior rows [r0, r0+R) (local rows of the model's slab; a sharded
 // slab needs 2 ghost rows of p' and 1 of rhs); all rows it needs — p' rows
-// r0-2..r0+R+1 and rhs rows r0-1..r0+R — are loaded up front, then
+// r0-2..r0+R+1 and rhs rows r0-1..r0+R — are read once, then
 //   red  rows r0-1..r0+R   from the old black neighbours (src),
 //   black rows r0..r0+R-1  from the new red ones (registers),
 // exactly the two color passes of k_sor_color over the same values: a red
@@ -110,115 +110,10 @@ __global__ __launch_bounds__(kBlock) void k_sor_color(float *__restrict__ pp,
 // only feed them, so waves step 62 pairs.  Iteration 0 reads no source: the
 // solve starts from p' = 0 (index.html:743).  The last segment of a column
 // ends at row_hi and overlaps its neighbour (identical stores).
-template <int FAST, int R>
-__global__ __launch_bounds__(kBlock) void k_sor_fused(const float *__restrict__ pa,
-                                                      const float *__restrict__ pb,
-                                                      float *__restrict__ qa, float *__restrict__ qb,
-                                                      const float *__restrict__ rhs, int nx, int ny,
-                                                      SorConst k, Ctl *ctl, uint32_t *err_slots,
-                                                      int pass, int it, int tol, float p_tol,
-                                                      int res, int nwc, int nseg, int row_lo,
-                                                      int row_hi, int j0, int lo_clamp,
-                                                      int hi_clamp) {
-    if (pass_off(ctl, pass)) return;
-    if (tol && it > 0 &&
-        read_max(err_slots + (size_t)(it - 1) * kResSlots * kResStride, ctl->err[it - 1]) < p_tol)
-        return;
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int lane = (int)threadIdx.x & 63;
-    const int bid = (int)blockIdx.x;
-    const int wc = bid % nwc;
-    const int seg = (bid / nwc) * (kBlock / 64) + wave;
-    if (seg >= nseg) return;   // wave-uniform
-    // buffers alternate per iteration from the solve's current one
-    const int si = (ctl->cur + it) & 1;
-    const float *__restrict__ src = si ? pb : pa;
-    float *__restrict__ dst = si ? qa : qb;
-    const int r0 = row_lo + min(seg * R, row_hi - row_lo - R);   // local rows
-    const int c = wc * 62 - 1 + lane;
-    const bool in_dom = c >= 0 && 2 * c < nx;
-    const bool out = in_dom && lane >= 1 && lane <= 62;
-    const int i0 = 2 * c;
-    float2 A[R + 4], Rh[R + 2];   // p' rows r0-2+q, rhs rows r0-1+q
-#pragma unroll
-    for (int q = 0; q < R + 4; ++q) {
-        const int r = min(max(r0 - 2 + q, lo_clamp), hi_clamp);
-        A[q] = (in_dom && it > 0) ? *reinterpret_cast<const float2 *>(src + (long)r * nx + i0)
-                                  : make_float2(0.0f, 0.0f);
-    }
-#pragma unroll
-    for (int q = 0; q < R + 2; ++q) {
-        const int r = min(max(r0 - 1 + q, lo_clamp), hi_clamp);
-        Rh[q] = in_dom ? *reinterpret_cast<const float2 *>(rhs + (long)r * nx + i0)
-                       : make_float2(0.0f, 0.0f);
-    }
-    const double omega = 1.7;
-    float m = 0.0f;
-    // one cell: the script's update (index.html:749-760) in double, stored as f32
-    auto relax = [&](float p_old_f, float pe, float pw, float pn, float ps, float rh, bool upd,
-                     bool count) {
-        if (!upd) return p_old_f;
-        const double p_old = (double)p_old_f;
-        const double h = ddiv<FAST>((double)pe + (double)pw, k.dx2, k.r_dx2);
-        const double v = ddiv<FAST>((double)pn + (double)ps, k.dy2, k.r_dy2);
-        const double p_update = ddiv<FAST>(h + v - (double)rh, k.denom, k.r_denom);
-        const float nv = (float)((1.0 - omega) * p_old + omega * p_update);
-        if (count) m = fmaxf(m, (float)fabs((double)nv - p_old));
-        return nv;
-    };
-    // red cells of rows r0-1+q (q = 0..R+1): column i0 + (row & 1)
-    float red[R + 2];
-#pragma unroll
-    for (int q = 0; q < R + 2; ++q) {
-        const int r = r0 - 1 + q;   // wave-uniform, local
-        const float2 a = A[q + 1], up = A[q + 2], dn = A[q];
-        const bool row_in = j0 + r >= 1 && j0 + r <= ny - 2;
-        const bool count = out && q >= 1 && q <= R;
-        if (((j0 + r) & 1) == 0) {   // red at x (column i0)
-            const int i = i0;
-            red[q] = relax(a.x, a.y, from_left(a.y), up.x, dn.x, Rh[q].x,
-                           row_in && i >= 1 && i <= nx - 2, count);
-        } else {              // red at y (column i0 + 1)
-            const int i = i0 + 1;
-            red[q] = relax(a.y, from_right(a.x), a.x, up.y, dn.y, Rh[q].y,
-                           row_in && i >= 1 && i <= nx - 2, count);
-        }
-    }
-    // black cells of rows r0+q (q = 0..R-1), the pair's final values, BCs
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const int r = r0 + q;
-        const float2 a = A[q + 2];
-        const float rd = red[q + 1];
-        float2 o;
-        if (((j0 + r) & 1) == 0) {   // red at x, black at y (column i0 + 1)
-            const int i = i0 + 1;
-            o.x = rd;
-            o.y = relax(a.y, from_right(rd), rd, red[q + 2], red[q], Rh[q + 1].y,
-                        i >= 1 && i <= nx - 2, out);
-        } else {              // black at x (column i0), red at y
-            const int i = i0;
-            o.y = rd;
-            o.x = relax(a.x, rd, from_left(rd), red[q + 2], red[q], Rh[q + 1].x,
-                        i >= 1 && i <= nx - 2, out);
-        }
-        if (i0 == 0) o.x = o.y;            // P(0,j) = P(1,j)
-        if (i0 + 1 == nx - 1) o.y = 0.0f;  // P(nx-1,j) = 0
-        if (out) {
-            *reinterpret_cast<float2 *>(dst + (long)r * nx + i0) = o;
-            if (j0 + r == 1) *reinterpret_cast<float2 *>(dst + (long)(r - 1) * nx + i0) = o;       // row 0
-            if (j0 + r == ny - 2) *reinterpret_cast<float2 *>(dst + (long)(r + 1) * nx + i0) = o;  // row ny-1
-        }
-    }
-    if (!res) return;
-    m = wave_max(out ? m : 0.0f);
-    if (lane == 0) publish_max(err_slots + (size_t)it * kResSlots * kResStride, bid * (kBlock / 64) + wave, m);
-}
-
-// k_sor_fused as a row march: the same updates in the same order, with the
-// p' and rhs rows streamed through register rings (prefetched PD steps
-// ahead) instead of all loaded up front, so a wave holds ~30 VGPRs of rows
-// instead of ~80 and more waves share each SIMD.  Step t (0..R+1) forms the
+// As a row march (r2; it replaced a form that loaded all of a segment's rows
+// up front, ~80 VGPRs of rows against ~30): the p' and rhs rows stream
+// through register rings (prefetched PD steps ahead), so more waves share
+// each SIMD.  Step t (0..R+1) forms the
 // red cells of row r0-1+t from p' rows r0-2+t..r0+t, then (t >= 2) the black
 // cells of row r0-2+t from the red rows of steps t-2..t and stores that row.
 template <int FAST, int R, int PD>
@@ -866,7 +761,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_final_residual(MgLevel L, const f
     }
 }
 
-// interior rows per k_sor_fused / k_sor_march segment: 32 where the slab has
+// interior rows per k_sor_march segment: 32 where the slab has
 // them (4096^2, 200 iterations: 9.02 ms; 8 rows 9.60, 16 rows 9.94, 64 rows
 // 13.45), else 16 (the minimum: sor_fused_ok)
 constexpr int kSorRows = 16, kSorRowsBig = 32;
@@ -900,36 +795,20 @@ void launch_sor_fused(float *pa, float *pb, const float *rhs, int nx, int ny, co
                       int row_lo, int row_hi, int j0, int lo_clamp, int hi_clamp, hipStream_t s) {
     const int nwc = cdiv(nx / 2, 62);
     const bool big = row_hi - row_lo >= kSorRowsBig;
-    int nseg = cdiv(row_hi - row_lo, big ? kSorRowsBig : kSorRows);
-    dim3 grid(nwc * cdiv(nseg, kBlock / 64));
-    // CFD_SOR_MARCH=0: the all-rows-up-front form
-    static const bool march = [] {
-        const char *e = getenv("CFD_SOR_MARCH");
-        return !(e && atoi(e) == 0);
-    }();
+    const int nseg = cdiv(row_hi - row_lo, big ? kSorRowsBig : kSorRows);
+    const dim3 grid(nwc * cdiv(nseg, kBlock / 64));
 #define CFD_LAUNCH_SOR(KER, FASTV, RR)                                                              \
     hipLaunchKernelGGL((KER<FASTV, RR>), grid, dim3(kBlock), 0, s, pa, pb, pa, pb, rhs,              \
                        nx, ny, k, ctl, err_slots, pass, it, tol, p_tol, res, nwc, nseg, row_lo,      \
                        row_hi, j0, lo_clamp, hi_clamp)
-    if (march) {
-        if (k.fast && big)
-            CFD_LAUNCH_SOR(k_sor_march, 1, kSorRowsBig);
-        else if (k.fast)
-            CFD_LAUNCH_SOR(k_sor_march, 1, kSorRows);
-        else if (big)
-            CFD_LAUNCH_SOR(k_sor_march, 0, kSorRowsBig);
-        else
-            CFD_LAUNCH_SOR(k_sor_march, 0, kSorRows);
-    } else {
-        // the all-rows-up-front form keeps 16-row segments
-        const int nseg16 = cdiv(row_hi - row_lo, kSorRows);
-        nseg = nseg16;
-        grid = dim3(nwc * cdiv(nseg, kBlock / 64));
-        if (k.fast)
-            CFD_LAUNCH_SOR(k_sor_fused, 1, kSorRows);
-        else
-            CFD_LAUNCH_SOR(k_sor_fused, 0, kSorRows);
-    }
+    if (k.fast && big)
+        CFD_LAUNCH_SOR(k_sor_march, 1, kSorRowsBig);
+    else if (k.fast)
+        CFD_LAUNCH_SOR(k_sor_march, 1, kSorRows);
+    else if (big)
+        CFD_LAUNCH_SOR(k_sor_march, 0, kSorRowsBig);
+    else
+        CFD_LAUNCH_SOR(k_sor_march, 0, kSorRows);
 #undef CFD_LAUNCH_SOR
 }
 
@@ -952,7 +831,7 @@ void launch_mg_smooth(const MgLevel &L, const float *src, float *dst, const Ctl 
 static int mg_smooth_mode() {
     // CFD_MG_SMOOTH: 1 the LDS block form, 2 the row march on every level,
     // 3 the wave windows on every level, 4 the march on levels of at least
-    // 2^CFD_MG_MARCH_MIN cells (default 22) and the windows below; default
+    // 2^22 cells and the windows below; default
     // (0): as 4 (4096^2 solve: windows 2.21, march everywhere 1.96, march
     // from 2^23 1.90, from 2^22 1.70, from 2^21 1.71 ms;
     // profiles/r2/mg/mgm2.log, mg_min_ab.log)
@@ -967,8 +846,7 @@ bool mg_smooth_wave_form() { return mg_smooth_mode() != 1; }
 static bool mg_use_march(const MgLevel &L) {
     const int m = mg_smooth_mode();
     if (m == 2) return true;
-    const char *mn = getenv("CFD_MG_MARCH_MIN");   // log2 cells of the smallest march level
-    const int lg = mn ? atoi(mn) : 22;
+    constexpr int lg = 22;   // log2 cells of the smallest march level
     return (m == 0 || m == 4) && (long)L.nx * L.ny >= (1L << lg);
 }
 

@@ -12,6 +12,8 @@ Since r4 the launch completes with any number of its workgroups resident
 than the GPU holds, and two models' launches running at once on one GPU are
 bitwise too.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -344,6 +346,74 @@ def test_persist_deadline_fault_on_slabs_recovers_every_rank(monkeypatch):
         for f in ("p_prime", "p", "rhs"):
             assert_bitwise(f"slab recovered {j0}:{f}", st[f], want[f].reshape(-1, nx)[j0:j1].ravel())
         assert_bitwise(f"slab recovered {j0}:u", st["u"], want["u"].reshape(-1, nx + 1)[j0:j1].ravel())
+
+@pytest.mark.timeout(300)
+def test_persist_deadline_fault_in_slab_pressure_solve(monkeypatch):
+    """cfd_pressure_solve on slabs with persistent runs and a forced deadline
+    fault: the entry point all-reduces the abort word itself
+    (no step all-reduce runs), so every rank reports CFD_ETIMEOUT, recovers
+    once and replays the same solve; p' then equals the single-domain
+    per-launch model's bit for bit."""
+    import threading
+    import cfdamd
+    from cfdamd._lib import CFD_ETIMEOUT, CfdError
+    n = 2
+    grid = cfdamd.cavity_grid(512, 1024)
+    params = cfdamd.SimulationParams.cavity(400.0, 200, corrector_passes=0, tol_enabled=False)
+    ref = cfdamd.Model(grid, params, device=0)
+    try:
+        ref.update_n(3)
+        ref.pressure_solve()
+        want = ref.get_state()
+    finally:
+        ref.close()
+    monkeypatch.setenv("CFD_HALO_DEPTH", "32")
+    monkeypatch.setenv("CFD_PERSIST_SHARDED", "1")
+    hub = cfdamd.LocalHub(n)
+    out, codes, models, errors = [None] * n, [None] * n, [None] * n, []
+    ready = threading.Barrier(n)
+
+    def worker(r):
+        try:
+            m = cfdamd.Model(grid, params, device=0, n_ranks=n, rank=r, local_hub=hub)
+            models[r] = m
+            m.update_n(3)
+            m.synchronize()
+            ready.wait(60)
+            if r == 0:
+                os.environ["CFD_PERSIST_DEADLINE_US"] = "0"   # every wait faults
+            ready.wait(60)
+            try:
+                m.pressure_solve()
+                m.synchronize()
+                codes[r] = 0
+            except CfdError as e:
+                codes[r] = e.code
+            out[r] = (m.get_state(), m.j0, m.j1, m.recoveries)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(n)]
+    try:
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(240)
+    finally:
+        os.environ.pop("CFD_PERSIST_DEADLINE_US", None)
+        for m in models:
+            if m is not None:
+                m.close()
+        hub.close()
+    if errors:
+        raise errors[0]
+    assert codes == [CFD_ETIMEOUT] * n, codes
+    nx = grid.nx
+    for st, j0, j1, rec in out:
+        assert rec == 1
+        assert_bitwise(f"slab solve recovered {j0}:p_prime", st["p_prime"],
+                       want["p_prime"].reshape(-1, nx)[j0:j1].ravel())
+
 
 def test_persist_off_under_graph_replay(monkeypatch):
     """CFD_GRAPH=1 replays captured steps with frozen kernel arguments, so
