@@ -55,7 +55,27 @@
 namespace cfd {
 namespace {
 
-constexpr int kResMaxT = 8;
+// sweeps per block between grid barriers: 10 since r6 (the reference
+// default's 50-sweep solves as 5 blocks instead of 6 + a 2-sweep tail:
+// 3.216 -> 3.050 ms per step; 9: 3.073, 13: 3.202; profiles/r6/prof_r6v,
+// prof_r6w)
+#ifndef CFD_RES_T
+#define CFD_RES_T 10
+#endif
+constexpr int kResMaxT = CFD_RES_T;
+
+// CFD_RES_STAMP (diagnostic builds only): thread 0 of workgroups 0..255
+// records s_memrealtime (100 MHz) at the phase boundaries of every block --
+// load start, load done, sweeps done, stores issued, stores drained, barrier
+// passed, residuals read -- in g_res_stamp (vector stores), read back by
+// cfd_diag_res_stamps (tools/res_stamps.py).  Off in the product build.
+#ifndef CFD_RES_STAMP
+#define CFD_RES_STAMP 0
+#endif
+constexpr int kResStampWG = 256, kResStampN = 64;
+#if CFD_RES_STAMP
+__device__ unsigned long long g_res_stamp[kResStampWG * kResStampN];
+#endif
 
 // WAVES: 8 (512 threads) or 16; ROWS: rows of one column a thread updates
 // per step of its loop (their LDS loads in flight together).  fin: the last workgroup out runs the solve's
@@ -95,6 +115,15 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
     const float omega = 0.75f;
     const float om1 = 1.0f - omega;
     const int cur0 = ctl->cur;
+    [[maybe_unused]] int nstamp = 0;
+    auto stamp = [&]() {
+#if CFD_RES_STAMP
+        if (threadIdx.x == 0 && wg < kResStampWG && nstamp < kResStampN)
+            g_res_stamp[wg * kResStampN + nstamp] = __builtin_amdgcn_s_memrealtime();
+        ++nstamp;
+#endif
+    };
+    stamp();
 
     // The tile's LDS region is its output cells plus a T-cell halo (clamped
     // to the grid), the same for every block, so with one tile per workgroup
@@ -116,6 +145,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
             const bool ld_rhs = !(keep_rhs && rhs_in);
             rhs_in = true;
             __syncthreads();   // the previous tile's LDS reads are done
+            stamp();
             {
                 // flat over the region, 4 loads in flight per thread before
                 // their LDS stores; row = idx / W by a float reciprocal (exact
@@ -143,6 +173,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
                 }
             }
             __syncthreads();
+            stamp();
             float *A = LA, *B = LB;
             const bool edge = r0 - T <= 0 || r1 + T >= ny || c0 - T <= 0 || c1 + T >= nx;
             for (int s = 0; s < Tb; ++s) {
@@ -223,6 +254,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
                 A = B;
                 B = tmp;
             }
+            stamp();
             // the tile's outputs, written through (sc1) for the other workgroups
             for (int r = r0 + wave; r < r1; r += kResWaves)
                 for (int c = c0 + lane; c < c1; c += 64)
@@ -245,6 +277,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
         if (threadIdx.x < kResWaves * kResMaxT) red_s[threadIdx.x / kResMaxT][threadIdx.x % kResMaxT] = 0.0f;
         __syncthreads();
         run_tiles(src, dst, Tb, publish);
+        stamp();
         __syncthreads();
         if (publish && (int)threadIdx.x < Tb && (g.tol_enabled || (int)threadIdx.x == Tb - 1)) {
             float m = 0.0f;
@@ -264,6 +297,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
         // ---- grid barrier: outputs and residual atomics drained, one arrival ----
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        stamp();
         if (threadIdx.x == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             int fail = 0;
@@ -310,6 +344,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
             flag_s = fail;
         }
         __syncthreads();
+        stamp();
         if (flag_s) {
             aborted = true;
             break;
@@ -320,6 +355,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_jacobi_resident(
             err_s[threadIdx.x] = __hip_atomic_load(&ctl->err[it + (int)threadIdx.x], __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
+        stamp();
         // the first sweep of the block below p_tol ends the solve (model.rs:816)
         int j = Tb;
         if (g.tol_enabled) {
@@ -465,6 +501,14 @@ bool launch_jacobi_resident(const Geom &g, const Fields &f, int pass, int iters,
 #undef CFD_RES_LAUNCH
     return true;
 }
+
+#if CFD_RES_STAMP
+extern "C" int cfd_diag_res_stamps(unsigned long long *host, int n) {
+    if (n > kResStampWG * kResStampN) n = kResStampWG * kResStampN;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_res_stamp), (size_t)n * 8, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
+#endif
 
 bool jacobi_resident_geometry(const Geom &g, int *br, int *bc, int *tiles, int *wgs) {
     // (the tile plan the launch would take; false: none fits)

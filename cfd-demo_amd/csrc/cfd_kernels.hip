@@ -1257,8 +1257,10 @@ __device__ __forceinline__ void cf4_row(const Geom &g, const Fields &f, const fl
 // of kCfRows rows: p' row lj, loaded for row lj, is row lj+1's lower neighbour
 // (the v correction's p'(j-1)), so every p' row crosses HBM once instead of
 // twice.
+// ROWS: the band (kCfRows, or 1 where the bands would leave the chip idle:
+// cf_rows).
 constexpr int kCfRows = 16;
-template <int SP>
+template <int SP, int ROWS>
 __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, float dt_override,
                                                              int nbx) {
     Ctl *c = f.ctl;
@@ -1267,7 +1269,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, f
     bool bad = false;
     const int bid = xcd_block(g);
     const int i0 = 4 * ((bid % nbx) * kBlock + (int)threadIdx.x);
-    const int l0 = (bid / nbx) * kCfRows, l1 = min(l0 + kCfRows, g.nyl + 1);
+    const int l0 = (bid / nbx) * ROWS, l1 = min(l0 + ROWS, g.nyl + 1);
     const float dt = dt_of(c, dt_override);
     const float inlet = c->inlet;
     const float *__restrict__ pp = c->cur ? f.pp[1] : f.pp[0];
@@ -1589,18 +1591,33 @@ bool correct_head_ok(const Geom &g, const Fields &f) {
            a16(f.pp[0]) && a16(f.pp[1]) && a16(f.rhs);
 }
 
+// Rows per thread of the corrector bands: kCfRows where that still gives
+// every CU two workgroups, else 1 (the 800 x 264 reference default: 17
+// workgroups of 16-row bands ran k_correct_head4 in 34.6 us against 5.9 us for
+// 270 one-row workgroups, profiles/r6/prof_r6u vs prof_r6l)
+static int cf_rows(const Geom &g, int nbx, int nrows) {
+    return (long)nbx * cdiv(nrows, kCfRows) >= 2L * g.n_cu ? kCfRows : 1;
+}
+
 void launch_correct_head(const Geom &g, const Fields &f, int pass, float dt_override, bool has_next,
                          hipStream_t s) {
     const int nbx4 = cdiv(g.nx / 4, kBlock);
     const int hn = has_next ? 1 : 0;
-    // the band march, kCfRows rows per thread (r6: C3 in the reference's control
-    // flow 10.37 -> 10.26 ms per step against one row per thread, best of 3;
-    // profiles/r6/prof_r6p/ab_corrhead.log)
-    const dim3 grid(nbx4 * cdiv(g.nyl + 1 + 2 * kGhostUV, kCfRows));
+    // the band march, kCfRows rows per thread, where it still fills the chip
+    // (r6: C3 in the reference's control flow 10.37 -> 10.26 ms per step
+    // against one row per thread, best of 3; profiles/r6/prof_r6p/ab_corrhead.log);
+    // on small grids one row per thread (cf_rows)
+    const int nrows = g.nyl + 1 + 2 * kGhostUV;
+    const int rows = cf_rows(g, nbx4, nrows);
+    const dim3 grid(nbx4 * cdiv(nrows, rows));
 #define CFD_LAUNCH_CH(SPV, RW)                                                                    \
     hipLaunchKernelGGL((k_correct_head4<SPV, RW>), grid, dim3(kBlock), 0, s, g, f, pass, dt_override, \
                        nbx4, hn)
-    if (g.sp_pow2) CFD_LAUNCH_CH(1, kCfRows); else CFD_LAUNCH_CH(0, kCfRows);
+    if (rows == kCfRows) {
+        if (g.sp_pow2) CFD_LAUNCH_CH(1, kCfRows); else CFD_LAUNCH_CH(0, kCfRows);
+    } else {
+        if (g.sp_pow2) CFD_LAUNCH_CH(1, 1); else CFD_LAUNCH_CH(0, 1);
+    }
 #undef CFD_LAUNCH_CH
 }
 
@@ -1608,11 +1625,16 @@ void launch_correct_finish(const Geom &g, const Fields &f, float dt_override, hi
     auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
     if (g.nx % 4 == 0 && a16(f.pp[0]) && a16(f.pp[1]) && a16(f.p) && a16(f.v) && a16(f.v_star)) {
         const int nbx = cdiv(g.nx / 4, kBlock);
-        const dim3 grid(nbx * cdiv(g.nyl + 1, kCfRows));
-        if (g.sp_pow2)
-            hipLaunchKernelGGL(k_correct_finish4m<1>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
-        else
-            hipLaunchKernelGGL(k_correct_finish4m<0>, grid, dim3(kBlock), 0, s, g, f, dt_override, nbx);
+        const int rows = cf_rows(g, nbx, g.nyl + 1);
+        const dim3 grid(nbx * cdiv(g.nyl + 1, rows));
+#define CFD_LAUNCH_CF(SPV, RW)                                                                     \
+    hipLaunchKernelGGL((k_correct_finish4m<SPV, RW>), grid, dim3(kBlock), 0, s, g, f, dt_override, nbx)
+        if (rows == kCfRows) {
+            if (g.sp_pow2) CFD_LAUNCH_CF(1, kCfRows); else CFD_LAUNCH_CF(0, kCfRows);
+        } else {
+            if (g.sp_pow2) CFD_LAUNCH_CF(1, 1); else CFD_LAUNCH_CF(0, 1);
+        }
+#undef CFD_LAUNCH_CF
         return;
     }
     const int nbx = cdiv(g.nx + 1, kBlock);
