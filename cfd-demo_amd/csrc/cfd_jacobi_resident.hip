@@ -431,8 +431,8 @@ int resident_blocks_per_cu(int lds) {
     return n;
 }
 
-// Tile shape: the candidate with the least LDS-box work per workgroup
-// (ceil(tiles / G) x box cells), every candidate admitting 2 workgroups per CU
+// Tile shape: the candidate with the least sweep work per workgroup
+// (ceil(tiles / G) x the lane slots of its T boxes), every candidate admitting 2 workgroups per CU
 // (one per CU in the grid, a margin of one).  Single domain only (rows
 // 0..ny-1 owned; the fields' ghost rows unused).  The occupancy queries are
 // cached; the rest is a few integer operations.
@@ -443,8 +443,11 @@ bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
     // reference default (800 x 264) took 32 x 48 (153 tiles, box 48 x 64);
     // 18 x 48 (255 tiles, box 34 x 64) runs the step 3.60 -> 3.23 ms
     // (profiles/r6/prof_r6i, prof_r6j)
-    static const int cand[][2] = {{8, 48},  {16, 48},  {18, 48},  {20, 48},
-                                  {24, 48}, {32, 48},  {16, 112}, {32, 112}};
+    // r6, T = 10: BC = 46 keeps every sweep's box (BC + 2e, e < T) in one
+    // 64-lane pass (48 needs two for e = 9)
+    static const int cand[][2] = {{8, 48},  {16, 48}, {18, 48}, {20, 48}, {24, 48},
+                                  {32, 48}, {19, 46}, {20, 46}, {22, 46}, {24, 46},
+                                  {16, 112}, {32, 112}};
     long best = -1;
     for (const auto &cd : cand) {
         const int BR = cd[0], BC = cd[1];
@@ -457,7 +460,11 @@ bool resident_plan(const Geom &g, int T, ResidentPlan *p) {
         const int tx = cdiv(g.nx, BC), ty = cdiv(g.ny, BR);
         const long nt = (long)tx * ty;
         const int G = (int)std::min<long>(nt, (long)g.n_cu);
-        const long work = (long)cdiv(nt, G) * (BR + 2 * T) * (BC + 2 * T);
+        // lane slots a workgroup's sweeps occupy: rows x 64-lane passes of
+        // each sweep's box
+        long slots = 0;
+        for (int e = 0; e < T; ++e) slots += (long)(BR + 2 * e) * 64 * cdiv(BC + 2 * e, 64);
+        const long work = (long)cdiv(nt, G) * slots;
         if (best < 0 || work < best) {
             best = work;
             *p = ResidentPlan{BR, BC, tx, (int)nt, G, lds};
