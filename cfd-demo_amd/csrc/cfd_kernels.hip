@@ -13,6 +13,10 @@
 
 namespace cfd {
 
+// 16 bytes at a 4-byte aligned address (the u rows' pitch nx + 1): one
+// global_load/store_dwordx4 (unaligned access mode) instead of four dwords
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+
 namespace {
 // Exhaustive proof of the fast forms for one divisor c (r = RN(1/c)):
 // counts inputs x where x*r (mode 1) or the corrected form (mode 2) differs
@@ -845,10 +849,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
             if (lr < nyl + kGhostUV) {   // not v's extra face row
                 const float *__restrict__ ur = f.u + ku;
                 float *__restrict__ us = f.u_star + ku;
-                us[0] = ur[0];
-                us[1] = ur[1];
-                us[2] = ur[2];
-                us[3] = ur[3];
+                *reinterpret_cast<f4u *>(us) = *reinterpret_cast<const f4u *>(ur);
                 if (i0 + 4 == nx) us[4] = ur[4];   // face nx
             }
         }
@@ -892,16 +893,15 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
         const float pr[5] = {pc.x, pc.y, pc.z, pc.w, p4};
         const float pw[5] = {pl, pc.x, pc.y, pc.z, pc.w};
         float un[5];
+        const f4u iu = *reinterpret_cast<const f4u *>(in_u + ku);   // dword-aligned (pitch nx + 1)
+        const float iuq[5] = {iu.x, iu.y, iu.z, iu.w, in_u[ku + 4]};
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
             const int i = i0 + q;
-            un[q] = (i >= 1 && i <= nx - 1) ? u_corr<SP>(g, in_u[ku + q], pr[q], pw[q], dt, i)
+            un[q] = (i >= 1 && i <= nx - 1) ? u_corr<SP>(g, iuq[q], pr[q], pw[q], dt, i)
                                             : f.u[ku + q];   // faces 0 and nx keep u
         }
-        out_u[ku] = un[0];
-        out_u[ku + 1] = un[1];
-        out_u[ku + 2] = un[2];
-        out_u[ku + 3] = un[3];
+        *reinterpret_cast<f4u *>(out_u + ku) = (f4u){un[0], un[1], un[2], un[3]};
         if (i0 + 4 == nx) out_u[ku + 4] = un[4];
         bool hit;
         const float4 vlo = carry ? v_next : v_row(lr, pc, &hit);
@@ -1191,8 +1191,10 @@ __device__ __forceinline__ void cf4_row(const Geom &g, const Fields &f, const fl
     if (lj < g.nyl) {
         const long k = (long)lj * W + i0;
         const float pl = (i0 > 0) ? pp[rp - 1] : 0.0f;
-        const float s0 = f.u_star[k], s1 = f.u_star[k + 1], s2 = f.u_star[k + 2],
-                    s3 = f.u_star[k + 3];
+        // u rows have pitch nx + 1: their 4-column groups are dword-aligned
+        // only, and move as one 16-byte access each (f4u)
+        const f4u su = *reinterpret_cast<const f4u *>(f.u_star + k);
+        const float s0 = su.x, s1 = su.y, s2 = su.z, s3 = su.w;
         float n0 = cf_u_face<SP>(g, inlet, dt, i0, j, s0, pc.x, pl);
         float n1 = cf_u_face<SP>(g, inlet, dt, i0 + 1, j, s1, pc.y, pc.x);
         float n2 = cf_u_face<SP>(g, inlet, dt, i0 + 2, j, s2, pc.z, pc.y);
@@ -1203,11 +1205,9 @@ __device__ __forceinline__ void cf4_row(const Geom &g, const Fields &f, const fl
             if (f.mask_u[k + 2] & 2) n2 = 0.0f;
             if (f.mask_u[k + 3] & 2) n3 = 0.0f;
         }
-        const float o0 = f.u[k], o1 = f.u[k + 1], o2 = f.u[k + 2], o3 = f.u[k + 3];
-        f.u[k] = n0;
-        f.u[k + 1] = n1;
-        f.u[k + 2] = n2;
-        f.u[k + 3] = n3;
+        const f4u uo = *reinterpret_cast<const f4u *>(f.u + k);
+        const float o0 = uo.x, o1 = uo.y, o2 = uo.z, o3 = uo.w;
+        *reinterpret_cast<f4u *>(f.u + k) = (f4u){n0, n1, n2, n3};
         du = fmaxf(fmaxf(fmaxf(du, fabsf(n0 - o0)), fmaxf(fabsf(n1 - o1), fabsf(n2 - o2))),
                    fabsf(n3 - o3));
         mu = fmaxf(fmaxf(fmaxf(mu, fabsf(n0)), fmaxf(fabsf(n1), fabsf(n2))), fabsf(n3));
