@@ -1259,7 +1259,10 @@ __device__ __forceinline__ void cf4_row(const Geom &g, const Fields &f, const fl
 // twice.
 // ROWS: the band (kCfRows, or 1 where the bands would leave the chip idle:
 // cf_rows).
-constexpr int kCfRows = 16;
+#ifndef CFD_CF_ROWS   // build-time (r6 A/B, profiles/r6/prof_r6ag: C3 16 / 8 / 4 rows
+#define CFD_CF_ROWS 16  // 10.04 / 10.36 / 10.18 ms per step)
+#endif
+constexpr int kCfRows = CFD_CF_ROWS;
 template <int SP, int ROWS>
 __global__ __launch_bounds__(kBlock) void k_correct_finish4m(Geom g, Fields f, float dt_override,
                                                              int nbx) {
