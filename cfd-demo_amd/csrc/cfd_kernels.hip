@@ -887,20 +887,27 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
             continue;
         }
         // ---- an owned row: corrector k, then pass k+1's copy and divergence
-        const float4 pc = carry ? p_next : *reinterpret_cast<const float4 *>(pp + kc);
-        const float pl = i0 > 0 ? pp[kc - 1] : 0.0f;
-        const float p4 = i0 + 4 < nx ? pp[kc + 4] : 0.0f;   // for the east face i0+4
+        // p' row lr: loaded every row (an L2 hit: it was row lr+1 of the last
+        // iteration) and the carried copy selected, so no branch guards the load
+        const float4 pld = *reinterpret_cast<const float4 *>(pp + kc);
+        const float4 pc = carry ? p_next : pld;
+        // every load unconditional (clamped in-row addresses) and the edge
+        // lanes' values selected afterwards: no lane-divergent branch around
+        // a load, so the row's loads stay in flight together
+        const float plv = pp[kc - (i0 > 0 ? 1 : 0)];
+        const float p4v = pp[kc + (i0 + 4 < nx ? 4 : 3)];
+        const float pl = i0 > 0 ? plv : 0.0f;
+        const float p4 = i0 + 4 < nx ? p4v : 0.0f;   // for the east face i0+4
         const float pr[5] = {pc.x, pc.y, pc.z, pc.w, p4};
         const float pw[5] = {pl, pc.x, pc.y, pc.z, pc.w};
         float un[5];
         const f4u iu = *reinterpret_cast<const f4u *>(in_u + ku);   // dword-aligned (pitch nx + 1)
         const float iuq[5] = {iu.x, iu.y, iu.z, iu.w, in_u[ku + 4]};
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const int i = i0 + q;
-            un[q] = (i >= 1 && i <= nx - 1) ? u_corr<SP>(g, iuq[q], pr[q], pw[q], dt, i)
-                                            : f.u[ku + q];   // faces 0 and nx keep u
-        }
+        for (int q = 0; q < 5; ++q) un[q] = u_corr<SP>(g, iuq[q], pr[q], pw[q], dt, i0 + q);
+        // faces 0 and nx keep u (the only lanes whose i0 + q leaves 1..nx-1)
+        if (i0 == 0) un[0] = f.u[ku];
+        if (i0 + 4 == nx) un[4] = f.u[ku + 4];
         *reinterpret_cast<f4u *>(out_u + ku) = (f4u){un[0], un[1], un[2], un[3]};
         if (i0 + 4 == nx) out_u[ku + 4] = un[4];
         bool hit;
