@@ -76,7 +76,7 @@ struct Ctl {
     uint32_t nonfinite_step;   // sticky: simulation_step after the first step whose
                                // velocities were not all finite (0 = never)
     uint32_t vis[2];        // render: max key, max ~key of the derived field (cfd_render.hip)
-    uint32_t done;          // workgroups finished (last-workgroup folds); 0 between launches
+    uint32_t done;          // (unused since r6: the last-workgroup folds were removed; keeps the layout)
     uint64_t sweeps_total;
     // speculative temporal blocking with the tolerance on (k_spec_check):
     // spec_stop: a launch of this solve converged (later launches skip);
