@@ -411,7 +411,16 @@ inline int resident_lds_bytes(int BR, int BC, int T) { return 3 * (BR + 2 * T) *
 // reference default 3.60 -> 3.23 ms per step at 18 x 48 tiles against 3.33
 // with 2 rows; 16-wave workgroups -1.5 %, not taken: profiles/r6/prof_r6j,
 // prof_r6m).
-constexpr int kResLaunchWaves = 8, kResLaunchRows = 1;
+// build-time (r6 A/B at T = 10, profiles/r6/prof_r6aj: 8 waves 1 row 3.031,
+// 2 rows 3.081 ms; 16 waves do not fit two workgroups per CU with this LDS
+// and fall back to the per-launch path, 7.32 ms)
+#ifndef CFD_RES_WAVES
+#define CFD_RES_WAVES 8
+#endif
+#ifndef CFD_RES_ROWS
+#define CFD_RES_ROWS 1
+#endif
+constexpr int kResLaunchWaves = CFD_RES_WAVES, kResLaunchRows = CFD_RES_ROWS;
 
 // Workgroups of the launched instantiation per CU with `lds` bytes of dynamic
 // LDS; cached per lds -- the plan is consulted on every tolerance-mode solve
