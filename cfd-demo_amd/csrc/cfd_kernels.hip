@@ -839,6 +839,28 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
     const int lr0 = (bid / nbx) * ROWS - kGhostUV, lr1 = min(lr0 + ROWS, nyl + 1 + kGhostUV);
     bool carry = false;          // p' row lr and v row lr from row lr-1's iteration
     float4 p_next = {0.f, 0.f, 0.f, 0.f}, v_next = {0.f, 0.f, 0.f, 0.f};
+    // an owned head row's loads: p' row r, its west / east neighbours (clamped
+    // in-row addresses, the edge lanes' values selected by the caller), u* row
+    // r, p' row r+1, v* row r+1 (v where row r+1 is not corrected), p row r
+    struct HRow {
+        float4 pld, pt, vsn, pv;
+        f4u iu;
+        float iu4, plv, p4v;
+    };
+    HRow cur, nxt;
+    bool have = false;   // cur holds row lr's loads
+    auto load_hrow = [&](int r, HRow &h) {
+        const long kc = (long)r * nx + i0, ku = (long)r * W + i0;
+        h.pld = *reinterpret_cast<const float4 *>(pp + kc);
+        h.plv = pp[kc - (i0 > 0 ? 1 : 0)];
+        h.p4v = pp[kc + (i0 + 4 < nx ? 4 : 3)];
+        h.iu = *reinterpret_cast<const f4u *>(in_u + ku);   // dword-aligned (pitch nx + 1)
+        h.iu4 = in_u[ku + 4];
+        h.pt = *reinterpret_cast<const float4 *>(pp + kc + nx);
+        const int jr = g.j0 + r + 1;   // model.rs:1366: v rows 1..ny-1 are corrected
+        h.vsn = *reinterpret_cast<const float4 *>((jr >= 1 && jr <= g.ny - 1 ? in_v : f.v) + kc + nx);
+        h.pv = *reinterpret_cast<const float4 *>(f.p + kc);
+    };
     for (int lr = lr0; lr < lr1; ++lr) {
         const long kc = (long)lr * nx + i0, ku = (long)lr * W + i0;
         const bool owned = lr >= 0 && lr < nyl;
@@ -855,6 +877,7 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
         }
         if (!owned && (head || lr != nyl)) {
             carry = false;
+            have = false;
             continue;
         }
         if (!head) {
@@ -884,25 +907,26 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
                 *reinterpret_cast<float4 *>(f.p + kc) = pv;
             }
             carry = false;
+            have = false;
             continue;
         }
         // ---- an owned row: corrector k, then pass k+1's copy and divergence
-        // p' row lr: loaded every row (an L2 hit: it was row lr+1 of the last
-        // iteration) and the carried copy selected, so no branch guards the load
-        const float4 pld = *reinterpret_cast<const float4 *>(pp + kc);
-        const float4 pc = carry ? p_next : pld;
-        // every load unconditional (clamped in-row addresses) and the edge
-        // lanes' values selected afterwards: no lane-divergent branch around
-        // a load, so the row's loads stay in flight together
-        const float plv = pp[kc - (i0 > 0 ? 1 : 0)];
-        const float p4v = pp[kc + (i0 + 4 < nx ? 4 : 3)];
-        const float pl = i0 > 0 ? plv : 0.0f;
-        const float p4 = i0 + 4 < nx ? p4v : 0.0f;   // for the east face i0+4
+        // Row lr's loads were issued during row lr-1 (cur) unless this is the
+        // band's first owned row; row lr+1's go out now, before row lr's
+        // stores (no array this row stores is one the next row loads at the
+        // same place), so each row's loads overlap the previous row's work.
+        if (!have) load_hrow(lr, cur);
+        const bool pf = ROWS > 1 && lr + 1 < lr1 && lr + 1 < nyl;   // the next row is owned too
+        if (pf) load_hrow(lr + 1, nxt);
+        // p' row lr: loaded every row and the carried copy selected, so no
+        // branch guards the load; the edge lanes' values selected likewise
+        const float4 pc = carry ? p_next : cur.pld;
+        const float pl = i0 > 0 ? cur.plv : 0.0f;
+        const float p4 = i0 + 4 < nx ? cur.p4v : 0.0f;   // for the east face i0+4
         const float pr[5] = {pc.x, pc.y, pc.z, pc.w, p4};
         const float pw[5] = {pl, pc.x, pc.y, pc.z, pc.w};
         float un[5];
-        const f4u iu = *reinterpret_cast<const f4u *>(in_u + ku);   // dword-aligned (pitch nx + 1)
-        const float iuq[5] = {iu.x, iu.y, iu.z, iu.w, in_u[ku + 4]};
+        const float iuq[5] = {cur.iu.x, cur.iu.y, cur.iu.z, cur.iu.w, cur.iu4};
 #pragma unroll
         for (int q = 0; q < 5; ++q) un[q] = u_corr<SP>(g, iuq[q], pr[q], pw[q], dt, i0 + q);
         // faces 0 and nx keep u (the only lanes whose i0 + q leaves 1..nx-1)
@@ -912,10 +936,20 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
         if (i0 + 4 == nx) out_u[ku + 4] = un[4];
         bool hit;
         const float4 vlo = carry ? v_next : v_row(lr, pc, &hit);
-        const float4 pt = *reinterpret_cast<const float4 *>(pp + kc + nx);
-        const float4 vhi = v_row(lr + 1, pt, &hit);
+        const float4 pt = cur.pt;
+        // v row lr+1 (v_row's expression; its p' row below is pc)
+        float4 vhi = cur.vsn;
+        {
+            const int jr = g.j0 + lr + 1;
+            if (jr >= 1 && jr <= g.ny - 1) {
+                vhi.x = cur.vsn.x - dt * sdiv<SP>(pt.x - pc.x, g.dy, g.r_dy);
+                vhi.y = cur.vsn.y - dt * sdiv<SP>(pt.y - pc.y, g.dy, g.r_dy);
+                vhi.z = cur.vsn.z - dt * sdiv<SP>(pt.z - pc.z, g.dy, g.r_dy);
+                vhi.w = cur.vsn.w - dt * sdiv<SP>(pt.w - pc.w, g.dy, g.r_dy);
+            }
+        }
         *reinterpret_cast<float4 *>(out_v + kc) = vlo;
-        float4 pv = *reinterpret_cast<const float4 *>(f.p + kc);
+        float4 pv = cur.pv;
         pv.x = pv.x + pc.x;
         pv.y = pv.y + pc.y;
         pv.z = pv.z + pc.z;
@@ -928,6 +962,8 @@ __global__ __launch_bounds__(kBlock) void k_correct_head4(Geom g, Fields f, int 
         r.z = (sdiv<SP>(un[3] - un[2], dx, rdx) + sdiv<SP>(vhi.z - vlo.z, dy, rdy)) / dt;
         r.w = (sdiv<SP>(un[4] - un[3], dx, rdx) + sdiv<SP>(vhi.w - vlo.w, dy, rdy)) / dt;
         *reinterpret_cast<float4 *>(f.rhs + kc) = r;
+        if (pf) cur = nxt;
+        have = pf;
         carry = ROWS > 1;
         p_next = pt;
         v_next = vhi;
