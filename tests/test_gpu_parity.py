@@ -378,6 +378,39 @@ def test_kernel_selection_rules(monkeypatch):
     m.close()
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("passes", [2, 3])
+def test_corrector_head_bands_full_width(monkeypatch, passes):
+    """The corrector head on a grid wide and tall enough for its 16-row bands
+    (cf_rows: 4096 x 2048 gives 4 x 129 = 516 workgroups >= 2 per CU) -- the
+    software-pipelined owned rows, the edge lanes' selected faces -- bitwise
+    against the separate corrector + copy + divergence launches
+    (CFD_CORR_HEAD=0), the loop ending on an even and on an odd pass; one step
+    also against the oracle."""
+    c = _cfd()
+    g = dict(nx=4096, ny=2048, lx=2.0, ly=1.0, cylinder=None)
+    kw = dict(bc_kind=1, viscosity=0.001, jacobi_iters=16, corrector_passes=passes, tol_enabled=False)
+    fields = ("u", "v", "p", "p_prime", "u_star", "v_star", "rhs")
+    got = {}
+    for env in ("0", "1"):
+        monkeypatch.setenv("CFD_CORR_HEAD", env)
+        m = c.Model(_grid(g), _params(kw))
+        try:
+            for _ in range(3):
+                m.update()
+            got[env] = m.get_state()
+        finally:
+            m.close()
+    for f in fields:
+        assert_bitwise(f"4096x2048 passes={passes} head bands vs separate:{f}", got["1"][f], got["0"][f])
+    if passes == 3:
+        o = _oracle(g, **kw)
+        for _ in range(3):
+            o.update()
+        for f in fields:
+            assert_bitwise(f"4096x2048 passes={passes} head bands vs oracle:{f}", got["1"][f], o.field(f))
+
+
 @pytest.mark.parametrize("passes,tol", [(1, False), (2, False), (3, False), (20, True)])
 def test_corrector_head_fused_matches_separate(monkeypatch, passes, tol):
     """k_correct_head4 (r4): the corrector of pass k with pass k+1's copy and
